@@ -1,0 +1,328 @@
+// extern "C" entry points declared in include/ecg.h.
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/ecg.h"
+#include "codes.hpp"
+#include "engine.hpp"
+
+using namespace ecg;
+
+struct ecg_ec {
+    ErasureCode* impl;
+};
+
+namespace {
+
+int* to_malloc(const std::vector<int>& v) {
+    if (v.empty()) return nullptr;
+    int* p = (int*)malloc(v.size() * sizeof(int));
+    if (p) memcpy(p, v.data(), v.size() * sizeof(int));
+    return p;
+}
+
+std::vector<int> vec(const int* p, int n) { return n > 0 && p ? std::vector<int>(p, p + n) : std::vector<int>(); }
+
+}  // namespace
+
+extern "C" {
+
+const char* ecg_last_error(void) { return last_error_string(); }
+int ecg_version(void) { return 100; }
+
+int ecg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ecg_set_device(int device) { return hipSetDevice(device) == hipSuccess ? ECG_OK : ECG_EHIP; }
+
+void ecg_free(void* p) { free(p); }
+
+// ------------------------------------------------------------------------------ tier 1
+
+int* ecg_reed_sol_vandermonde_coding_matrix(int k, int m, int w) {
+    if (w != 8) return nullptr;
+    return to_malloc(reed_sol_vandermonde_coding_matrix(k, m));
+}
+
+int* ecg_cauchy_good_general_coding_matrix(int k, int m, int w) {
+    if (w != 8) return nullptr;
+    return to_malloc(cauchy_good_general_coding_matrix(k, m));
+}
+
+int* ecg_cauchy_original_coding_matrix(int k, int m, int w) {
+    if (w != 8) return nullptr;
+    return to_malloc(cauchy_original_coding_matrix(k, m));
+}
+
+void ecg_cauchy_improve_coding_matrix(int k, int m, int w, int* matrix) {
+    if (w != 8 || !matrix || k < 1 || m < 1) return;
+    std::vector<int> M(matrix, matrix + (size_t)k * m);
+    cauchy_improve_coding_matrix(k, m, M);
+    memcpy(matrix, M.data(), M.size() * sizeof(int));
+}
+
+int ecg_cauchy_n_ones(int n, int w) { return w == 8 ? cauchy_n_ones(n) : -1; }
+
+int ecg_jerasure_invert_matrix(int* mat, int* inv, int rows, int w) {
+    if (w != 8 || rows < 1 || !mat || !inv) return -1;
+    std::vector<int> a(mat, mat + (size_t)rows * rows), b;
+    const int rc = invert_matrix(a, b, rows);
+    memcpy(mat, a.data(), a.size() * sizeof(int));  // the library works in place on `mat`
+    memcpy(inv, b.data(), b.size() * sizeof(int));
+    return rc;
+}
+
+int* ecg_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int c2, int w) {
+    if (w != 8 || !m1 || !m2 || r1 < 1 || c2 < 1) return nullptr;
+    return to_malloc(matrix_multiply(m1, m2, r1, c1, r2, c2));
+}
+
+int ecg_galois_region_xor(char* src, char* dest, int nbytes) {
+    if (nbytes < 0 || !src || !dest) return ECG_EINVAL;
+    LinearOp op;
+    op.src_ids = {0, 1};
+    op.dst_ids = {1};
+    op.coef = {1, 1};
+    uint8_t* blocks[2] = {(uint8_t*)src, (uint8_t*)dest};
+    return Engine::instance().run_host({op}, blocks, 2, nbytes);
+}
+
+int ecg_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs, int size) {
+    if (w != 8 || k < 1 || m < 1 || !matrix || size < 0) return ECG_EINVAL;
+    LinearOp op = plan_matrix_encode(k, m, matrix);
+    if (op.m_out() == 0) return ECG_OK;
+    std::vector<uint8_t*> blocks((size_t)k + m);
+    for (int i = 0; i < k; i++) blocks[i] = (uint8_t*)data_ptrs[i];
+    for (int i = 0; i < m; i++) blocks[(size_t)k + i] = (uint8_t*)coding_ptrs[i];
+    return Engine::instance().run_host({op}, blocks.data(), k + m, size);
+}
+
+int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
+                               char** coding_ptrs, int size) {
+    if (w != 8 || k < 1 || m < 1 || !matrix || !erasures || size < 0) return -1;
+    std::vector<LinearOp> ops;
+    if (plan_matrix_decode(k, m, matrix, row_k_ones, erasures, ops) < 0) return -1;
+    std::vector<uint8_t*> blocks((size_t)k + m);
+    for (int i = 0; i < k; i++) blocks[i] = (uint8_t*)data_ptrs[i];
+    for (int i = 0; i < m; i++) blocks[(size_t)k + i] = (uint8_t*)coding_ptrs[i];
+    const int rc = Engine::instance().run_host(ops, blocks.data(), k + m, size);
+    return rc == ECG_OK ? 0 : rc;
+}
+
+// ------------------------------------------------------------------------------ tier 2
+
+int ecg_dev_matrix_encode(int k, int m, const int* matrix, char** d_data_ptrs, char** d_coding_ptrs, long long B,
+                          void* stream) {
+    if (k < 1 || m < 1 || !matrix || B < 0) return ECG_EINVAL;
+    LinearOp op = plan_matrix_encode(k, m, matrix);
+    if (op.m_out() == 0) return ECG_OK;
+    std::vector<uint8_t*> blocks((size_t)k + m);
+    for (int i = 0; i < k; i++) blocks[i] = (uint8_t*)d_data_ptrs[i];
+    for (int i = 0; i < m; i++) blocks[(size_t)k + i] = (uint8_t*)d_coding_ptrs[i];
+    return Engine::instance().run_device({op}, blocks.data(), k + m, B, (hipStream_t)stream);
+}
+
+int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const int* erasures, char** d_data_ptrs,
+                          char** d_coding_ptrs, long long B, void* stream) {
+    if (k < 1 || m < 1 || !matrix || !erasures || B < 0) return ECG_EINVAL;
+    std::vector<LinearOp> ops;
+    if (plan_matrix_decode(k, m, matrix, row_k_ones, erasures, ops) < 0) return ECG_EUNDECODABLE;
+    std::vector<uint8_t*> blocks((size_t)k + m);
+    for (int i = 0; i < k; i++) blocks[i] = (uint8_t*)d_data_ptrs[i];
+    for (int i = 0; i < m; i++) blocks[(size_t)k + i] = (uint8_t*)d_coding_ptrs[i];
+    return Engine::instance().run_device(ops, blocks.data(), k + m, B, (hipStream_t)stream);
+}
+
+int ecg_matrix_apply_batch(int k_in, int m_out, const int* coef, const int* src_ids, const int* dst_ids,
+                           const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
+                           long long out_sstride, long long out_bstride, long long B, int S, void* stream) {
+    if (k_in < 1 || m_out < 1 || !coef || !src_ids || !dst_ids) return ECG_EINVAL;
+    LinearOp op;
+    op.src_ids = vec(src_ids, k_in);
+    op.dst_ids = vec(dst_ids, m_out);
+    op.coef.resize((size_t)k_in * m_out);
+    for (size_t i = 0; i < op.coef.size(); i++) op.coef[i] = (uint8_t)(coef[i] & 0xff);
+    return Engine::instance().run_strided({op}, nullptr, S, in_base, in_sstride, in_bstride, out_base, out_sstride,
+                                          out_bstride, B, (hipStream_t)stream);
+}
+
+int ecg_encode_batch(int k, int m, const int* matrix, const void* d_in, long long in_sstride, long long in_bstride,
+                     void* d_out, long long out_sstride, long long out_bstride, long long B, int S, void* stream) {
+    if (k < 1 || m < 1 || !matrix) return ECG_EINVAL;
+    LinearOp op = plan_matrix_encode(k, m, matrix);
+    if (op.m_out() == 0) return ECG_OK;
+    for (int& d : op.dst_ids) d -= k;  // coding block i -> out block i
+    return Engine::instance().run_strided({op}, nullptr, S, d_in, in_sstride, in_bstride, d_out, out_sstride,
+                                          out_bstride, B, (hipStream_t)stream);
+}
+
+int ecg_decode_batch(int k, int m, const int* matrix, int row_k_ones, const int* patterns, int n_patterns,
+                     const int* d_pattern_of_stripe, void* d_stripes, long long sstride, long long bstride,
+                     void* d_out, long long out_sstride, long long out_bstride, long long B, int S, void* stream) {
+    if (k < 1 || m < 1 || !matrix || !patterns || n_patterns < 1) return ECG_EINVAL;
+    if (n_patterns > 1 && !d_pattern_of_stripe) return ECG_EINVAL;
+    std::vector<LinearOp> progs;
+    const int* pat = patterns;
+    for (int p = 0; p < n_patterns; p++) {
+        std::vector<LinearOp> ops;
+        if (plan_matrix_decode(k, m, matrix, row_k_ones, pat, ops) < 0) return ECG_EUNDECODABLE;
+        if (ops.size() != 1) return ECG_EINVAL;  // non-composable pattern: use ecg_dev_matrix_decode
+        if (d_out)
+            for (size_t i = 0; i < ops[0].dst_ids.size(); i++) ops[0].dst_ids[i] = (int)i;
+        if (!progs.empty() && (ops[0].k_in() != progs[0].k_in() || ops[0].m_out() != progs[0].m_out()))
+            return ECG_EINVAL;
+        progs.push_back(std::move(ops[0]));
+        while (*pat != -1) pat++;
+        pat++;
+    }
+    void* out = d_out ? d_out : d_stripes;
+    return Engine::instance().run_strided(progs, d_pattern_of_stripe, S, d_stripes, sstride, bstride, out,
+                                          d_out ? out_sstride : sstride, d_out ? out_bstride : bstride, B,
+                                          (hipStream_t)stream);
+}
+
+int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, long long in_sstride,
+                               long long in_bstride, void* d_out, long long out_sstride, long long out_bstride,
+                               long long B, int S, void* stream) {
+    if (parity_num < 1 || block_num < 1 || block_num % parity_num != 0) return ECG_EINVAL;
+    LinearOp op;
+    for (int j = 0; j < block_num; j++) op.src_ids.push_back(j);
+    for (int i = 0; i < parity_num; i++) op.dst_ids.push_back(i);
+    op.coef.assign((size_t)block_num * parity_num, 0);
+    for (int i = 0; i < parity_num; i++)
+        for (int j = 0; j < block_num / parity_num; j++) op.coef[(size_t)i * block_num + j * parity_num + i] = 1;
+    return Engine::instance().run_strided({op}, nullptr, S, d_in, in_sstride, in_bstride, d_out, out_sstride,
+                                          out_bstride, B, (hipStream_t)stream);
+}
+
+int ecg_fill_random(void* d_dst, long long nbytes, unsigned long long seed, unsigned long long word_offset,
+                    void* stream) {
+    if (!d_dst || nbytes < 0) return ECG_EINVAL;
+    hipError_t e = launch_fill_splitmix(d_dst, nbytes, seed, word_offset, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        set_last_error(std::string("fill: ") + hipGetErrorString(e));
+        return ECG_EHIP;
+    }
+    return ECG_OK;
+}
+
+// ------------------------------------------------------------------------------ tier 3
+
+ecg_ec* ecg_ec_factory(int ec_type, const ecg_coding_parameters* cp) {
+    if (!cp) return nullptr;
+    ErasureCode* impl = ec_factory(ec_type, *cp);
+    if (!impl) return nullptr;
+    return new ecg_ec{impl};
+}
+
+void ecg_ec_destroy(ecg_ec* ec) {
+    if (!ec) return;
+    delete ec->impl;
+    delete ec;
+}
+
+int ecg_ec_init_coding_parameters(ecg_ec* ec, const ecg_coding_parameters* cp) {
+    if (!ec || !cp) return ECG_EINVAL;
+    ec->impl->init_coding_parameters(*cp);
+    return ECG_OK;
+}
+
+int ecg_ec_get_coding_parameters(ecg_ec* ec, ecg_coding_parameters* cp) {
+    if (!ec || !cp) return ECG_EINVAL;
+    ec->impl->get_coding_parameters(*cp);
+    return ECG_OK;
+}
+
+int ecg_ec_set_memory(ecg_ec* ec, int mem, void* stream) {
+    if (!ec || (mem != ECG_MEM_HOST && mem != ECG_MEM_DEVICE)) return ECG_EINVAL;
+    ec->impl->mem = mem;
+    ec->impl->stream = (hipStream_t)stream;
+    return ECG_OK;
+}
+
+int ecg_ec_set_isvertical(ecg_ec* ec, int isvertical) {
+    if (!ec) return ECG_EINVAL;
+    HPC* h = dynamic_cast<HPC*>(ec->impl);
+    if (!h) return ECG_EINVAL;
+    h->isvertical = isvertical != 0;
+    return ECG_OK;
+}
+
+int ecg_ec_k(const ecg_ec* ec) { return ec ? ec->impl->k : ECG_EINVAL; }
+int ecg_ec_m(const ecg_ec* ec) { return ec ? ec->impl->m : ECG_EINVAL; }
+
+int ecg_ec_make_encoding_matrix(ecg_ec* ec, int* final_matrix) {
+    if (!ec || !final_matrix) return ECG_EINVAL;
+    return ec->impl->make_encoding_matrix(final_matrix);
+}
+
+int ecg_ec_check_if_decodable(ecg_ec* ec, const int* failure_idxs, int n) {
+    if (!ec || n < 0) return ECG_EINVAL;
+    return ec->impl->check_if_decodable(vec(failure_idxs, n));
+}
+
+int ecg_ec_encode(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size) {
+    if (!ec || !data_ptrs || !coding_ptrs || block_size < 0) return ECG_EINVAL;
+    return ec->impl->encode(data_ptrs, coding_ptrs, block_size);
+}
+
+int ecg_ec_decode(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) {
+    if (!ec || !data_ptrs || !coding_ptrs || !erasures || block_size < 0 || failed_num < 0) return ECG_EINVAL;
+    return ec->impl->decode(data_ptrs, coding_ptrs, block_size, erasures, failed_num);
+}
+
+int ecg_ec_encode_partial_blocks_for_encoding(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size,
+                                              const int* data_idxs, int n_data, const int* parity_idxs,
+                                              int n_parity) {
+    if (!ec || n_data < 1 || n_parity < 1 || block_size < 0) return ECG_EINVAL;
+    return ec->impl->encode_partial_blocks_for_encoding(data_ptrs, coding_ptrs, block_size, vec(data_idxs, n_data),
+                                                        vec(parity_idxs, n_parity));
+}
+
+int ecg_ec_encode_partial_blocks_for_decoding(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size,
+                                              const int* local_survivor_idxs, int n_local,
+                                              const int* survivor_idxs, int n_survivors,
+                                              const int* failure_idxs, int n_failures) {
+    if (!ec || n_local < 1 || n_survivors < 1 || n_failures < 1 || block_size < 0) return ECG_EINVAL;
+    return ec->impl->encode_partial_blocks_for_decoding(data_ptrs, coding_ptrs, block_size,
+                                                        vec(local_survivor_idxs, n_local),
+                                                        vec(survivor_idxs, n_survivors),
+                                                        vec(failure_idxs, n_failures));
+}
+
+int ecg_ec_perform_addition(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size, int block_num,
+                            int parity_num) {
+    if (!ec || block_size < 0) return ECG_EINVAL;
+    return ec->impl->perform_addition(data_ptrs, coding_ptrs, block_size, block_num, parity_num);
+}
+
+int ecg_ec_partial_decoding_matrix(ecg_ec* ec, const int* local_survivor_idxs, int n_local,
+                                   const int* survivor_idxs, int n_survivors, const int* failure_idxs,
+                                   int n_failures, int* out_coef, int out_cap) {
+    if (!ec || !out_coef) return ECG_EINVAL;
+    std::vector<int> M;
+    int rc = ec->impl->partial_decoding_matrix(vec(local_survivor_idxs, n_local), vec(survivor_idxs, n_survivors),
+                                               vec(failure_idxs, n_failures), M);
+    if (rc != ECG_OK) return rc;
+    if ((int)M.size() > out_cap) return ECG_EINVAL;
+    memcpy(out_coef, M.data(), M.size() * sizeof(int));
+    return n_failures;
+}
+
+int ecg_ec_partial_encoding_matrix(ecg_ec* ec, const int* data_idxs, int n_data, const int* parity_idxs,
+                                   int n_parity, int* out_coef, int out_cap) {
+    if (!ec || !out_coef) return ECG_EINVAL;
+    std::vector<int> M;
+    int rc = ec->impl->partial_encoding_matrix(vec(data_idxs, n_data), vec(parity_idxs, n_parity), M);
+    if (rc != ECG_OK) return rc;
+    if ((int)M.size() > out_cap) return ECG_EINVAL;
+    memcpy(out_coef, M.data(), M.size() * sizeof(int));
+    return n_parity;
+}
+
+}  // extern "C"

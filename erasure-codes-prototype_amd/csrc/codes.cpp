@@ -1,0 +1,1040 @@
+// ErasureCode facade implementation.  Each method cites the reference lines it mirrors
+// (paths relative to /root/reference/project).
+#include "codes.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+
+#include "engine.hpp"
+#include "gf256.hpp"
+
+namespace ecg {
+
+// ================================================================================== plan helpers
+
+static void remap(LinearOp& op, int k, const std::vector<int>& data_ids, const std::vector<int>& coding_ids) {
+    auto f = [&](int id) { return id < k ? data_ids[id] : coding_ids[id - k]; };
+    for (int& id : op.src_ids) id = f(id);
+    for (int& id : op.dst_ids) id = f(id);
+}
+
+void append_encode(Plan& plan, int k, int m, const int* matrix, const std::vector<int>& data_ids,
+                   const std::vector<int>& coding_ids) {
+    LinearOp op = plan_matrix_encode(k, m, matrix);
+    if (op.m_out() == 0) return;
+    remap(op, k, data_ids, coding_ids);
+    plan.ops.push_back(std::move(op));
+}
+
+int append_decode(Plan& plan, int k, int m, const int* matrix, int row_k_ones, const int* erasures,
+                  const std::vector<int>& data_ids, const std::vector<int>& coding_ids) {
+    std::vector<LinearOp> ops;
+    if (plan_matrix_decode(k, m, matrix, row_k_ones, erasures, ops) < 0) return ECG_EUNDECODABLE;
+    for (LinearOp& op : ops) {
+        remap(op, k, data_ids, coding_ids);
+        plan.ops.push_back(std::move(op));
+    }
+    return ECG_OK;
+}
+
+static std::vector<int> iota_ids(int n, int base = 0) {
+    std::vector<int> v(n);
+    for (int i = 0; i < n; i++) v[i] = base + i;
+    return v;
+}
+
+// ================================================================================== ErasureCode
+
+void ErasureCode::init_coding_parameters(const CodingParameters& cp) {  // erasure_code.cpp:5-10
+    k = cp.k;
+    m = cp.m;
+    local_or_column = cp.local_or_column != 0;
+}
+
+void ErasureCode::get_coding_parameters(CodingParameters& cp) const {  // erasure_code.cpp:12-17
+    cp.k = k;
+    cp.m = m;
+    cp.local_or_column = local_or_column;
+}
+
+void ErasureCode::get_full_matrix(int* matrix, int kk) {  // erasure_code.cpp:30-35
+    for (int i = 0; i < kk; i++) matrix[(size_t)i * kk + i] = 1;
+}
+
+void ErasureCode::make_submatrix_by_rows(int cols, const int* matrix, int* new_matrix,
+                                         const std::vector<int>& idxs) {  // erasure_code.cpp:37-47
+    for (size_t i = 0; i < idxs.size(); i++)
+        memcpy(&new_matrix[i * cols], &matrix[(size_t)idxs[i] * cols], (size_t)cols * sizeof(int));
+}
+
+void ErasureCode::make_submatrix_by_cols(int cols, int rows, const int* matrix, int* new_matrix,
+                                         const std::vector<int>& idxs) {  // erasure_code.cpp:49-61
+    const int n = (int)idxs.size();
+    for (int i = 0; i < n; i++)
+        for (int u = 0; u < rows; u++) new_matrix[(size_t)u * n + i] = matrix[(size_t)u * cols + idxs[i]];
+}
+
+// erasure_code.cpp:97-111 (the matrix handed to jerasure_matrix_encode)
+void ErasureCode::partial_encoding_matrix_(int k_, const int* full, const std::vector<int>& data_idxs,
+                                           const std::vector<int>& parity_idxs, std::vector<int>& out) {
+    const int nb = (int)data_idxs.size(), np = (int)parity_idxs.size();
+    std::vector<int> rows((size_t)np * k_, 0);
+    make_submatrix_by_rows(k_, full, rows.data(), parity_idxs);
+    out.assign((size_t)np * nb, 1);
+    make_submatrix_by_cols(k_, np, rows.data(), out.data(), data_idxs);
+}
+
+// erasure_code.cpp:113-150: R = F[failures] * inv(F[survivors]); columns of the local survivors.
+void ErasureCode::partial_decoding_matrix_(int k_, const int* full, const std::vector<int>& lsi,
+                                           const std::vector<int>& si, const std::vector<int>& fi,
+                                           std::vector<int>& out) {
+    const int nl = (int)lsi.size(), nf = (int)fi.size();
+    std::vector<int> fm((size_t)nf * k_, 0), sm((size_t)k_ * k_, 0), inv;
+    make_submatrix_by_rows(k_, full, fm.data(), fi);
+    make_submatrix_by_rows(k_, full, sm.data(), si);
+    (void)invert_matrix(sm, inv, k_);  // return value ignored, erasure_code.cpp:128
+    std::vector<int> dec = matrix_multiply(fm.data(), inv.data(), nf, k_, k_, k_);
+    out.assign((size_t)nf * nl, 0);
+    for (int i = 0; i < nl; i++) {
+        int idx = 0;
+        for (int s : si) {
+            if (s == lsi[i]) break;
+            idx++;
+        }
+        for (int u = 0; u < nf; u++) {
+            const size_t at = (size_t)u * k_ + idx;
+            out[(size_t)u * nl + i] = at < dec.size() ? dec[at] : 0;
+        }
+    }
+}
+
+int ErasureCode::run(const Plan& plan, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding,
+                     long long B) {
+    if (plan.ops.empty()) return ECG_OK;
+    std::vector<uint8_t*> blocks((size_t)n_data + n_coding, nullptr);
+    for (int i = 0; i < n_data; i++) blocks[i] = (uint8_t*)data_ptrs[i];
+    for (int i = 0; i < n_coding; i++) blocks[(size_t)n_data + i] = (uint8_t*)coding_ptrs[i];
+    Engine& eng = Engine::instance();
+    if (mem == ECG_MEM_DEVICE) return eng.run_device(plan.ops, blocks.data(), (int)blocks.size(), B, stream);
+    return eng.run_host(plan.ops, blocks.data(), (int)blocks.size(), B);
+}
+
+int ErasureCode::run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B) {
+    Plan p;
+    append_encode(p, kk, mm, matrix, iota_ids(kk), iota_ids(mm, kk));
+    return run(p, data_ptrs, kk, coding_ptrs, mm, B);
+}
+
+int ErasureCode::run_decode(int kk, int mm, const int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
+                            char** coding_ptrs, long long B) {
+    Plan p;
+    int rc = append_decode(p, kk, mm, matrix, row_k_ones, erasures, iota_ids(kk), iota_ids(mm, kk));
+    if (rc != ECG_OK) return rc;
+    return run(p, data_ptrs, kk, coding_ptrs, mm, B);
+}
+
+int ErasureCode::encode_partial_blocks_for_encoding(char** data_ptrs, char** coding_ptrs, int block_size,
+                                                    std::vector<int> data_idxs, std::vector<int> parity_idxs) {
+    std::vector<int> M;
+    const int nd = (int)data_idxs.size(), np = (int)parity_idxs.size();
+    int rc = partial_encoding_matrix(std::move(data_idxs), std::move(parity_idxs), M);
+    if (rc != ECG_OK) return rc;
+    return run_encode(nd, np, M.data(), data_ptrs, coding_ptrs, block_size);
+}
+
+int ErasureCode::encode_partial_blocks_for_decoding(char** data_ptrs, char** coding_ptrs, int block_size,
+                                                    std::vector<int> lsi, std::vector<int> si,
+                                                    std::vector<int> fi) {
+    std::vector<int> M;
+    const int nl = (int)lsi.size(), nf = (int)fi.size();
+    int rc = partial_decoding_matrix(std::move(lsi), std::move(si), std::move(fi), M);
+    if (rc != ECG_OK) return rc;
+    return run_encode(nl, nf, M.data(), data_ptrs, coding_ptrs, block_size);
+}
+
+// erasure_code.cpp:70-94: coding[i] = XOR_j data[j * parity_num + i], one launch for all i.
+int ErasureCode::perform_addition(char** data_ptrs, char** coding_ptrs, int block_size, int block_num,
+                                  int parity_num) {
+    if (parity_num <= 0 || block_num < 0 || block_num % parity_num != 0) return ECG_EINVAL;
+    if (block_num == 0) return ECG_OK;
+    LinearOp op;
+    op.src_ids = iota_ids(block_num);
+    op.dst_ids = iota_ids(parity_num, block_num);
+    op.coef.assign((size_t)parity_num * block_num, 0);
+    const int per = block_num / parity_num;
+    for (int i = 0; i < parity_num; i++)
+        for (int j = 0; j < per; j++) op.coef[(size_t)i * block_num + (size_t)j * parity_num + i] = 1;
+    Plan p;
+    p.ops.push_back(std::move(op));
+    return run(p, data_ptrs, block_num, coding_ptrs, parity_num, block_size);
+}
+
+static bool ids_in_range(const std::vector<int>& v, int n) {
+    for (int x : v)
+        if (x < 0 || x >= n) return false;
+    return true;
+}
+
+// ================================================================================== RS / ERS
+
+const std::vector<int>& RSCode::vandermonde() {
+    if (vand_k_ != k || vand_m_ != m) {
+        vand_ = reed_sol_vandermonde_coding_matrix(k, m);
+        vand_k_ = k;
+        vand_m_ = m;
+    }
+    return vand_;
+}
+
+int RSCode::make_encoding_matrix(int* final_matrix) {  // rs.cpp:5-18
+    const std::vector<int>& v = vandermonde();
+    if (v.empty()) return ECG_EINVAL;
+    std::copy(v.begin(), v.end(), final_matrix);
+    return ECG_OK;
+}
+
+std::vector<int> RSCode::full_matrix() {  // rs.cpp:48-50
+    std::vector<int> f((size_t)(k + m) * k, 0);
+    get_full_matrix(f.data(), k);
+    make_encoding_matrix(&f[(size_t)k * k]);
+    return f;
+}
+
+int RSCode::encode(char** data_ptrs, char** coding_ptrs, int block_size) {  // rs.cpp:20-25
+    std::vector<int> M((size_t)k * m, 0);
+    int rc = make_encoding_matrix(M.data());
+    if (rc != ECG_OK) return rc;
+    return run_encode(k, m, M.data(), data_ptrs, coding_ptrs, block_size);
+}
+
+// rs.cpp:27-42.  NB: decodes with reed_sol_vandermonde_coding_matrix(k, m) even for EnlargedRSCode,
+// and passes failed_num as row_k_ones, exactly like the reference.
+int RSCode::decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) {
+    if (failed_num > m) return ECG_EUNDECODABLE;
+    const std::vector<int>& v = vandermonde();
+    if (v.empty()) return ECG_EINVAL;
+    return run_decode(k, m, v.data(), failed_num, erasures, data_ptrs, coding_ptrs, block_size);
+}
+
+int RSCode::plan_encode(Plan& p, const std::vector<int>& data_ids, const std::vector<int>& coding_ids) {
+    std::vector<int> M((size_t)k * m, 0);
+    int rc = make_encoding_matrix(M.data());
+    if (rc != ECG_OK) return rc;
+    append_encode(p, k, m, M.data(), data_ids, coding_ids);
+    return ECG_OK;
+}
+
+int RSCode::plan_decode(Plan& p, const std::vector<int>& data_ids, const std::vector<int>& coding_ids,
+                        int* erasures, int failed_num) {
+    if (failed_num > m) return ECG_EUNDECODABLE;
+    const std::vector<int>& v = vandermonde();
+    if (v.empty()) return ECG_EINVAL;
+    return append_decode(p, k, m, v.data(), failed_num, erasures, data_ids, coding_ids);
+}
+
+int RSCode::check_if_decodable(const std::vector<int>& f) { return m >= (int)f.size() ? 1 : 0; }  // rs.cpp:68-76
+
+int RSCode::partial_encoding_matrix(std::vector<int> data_idxs, std::vector<int> parity_idxs,
+                                    std::vector<int>& out) {  // rs.cpp:44-53
+    if (!ids_in_range(data_idxs, k) || !ids_in_range(parity_idxs, k + m)) return ECG_EINVAL;
+    std::vector<int> f = full_matrix();
+    partial_encoding_matrix_(k, f.data(), data_idxs, parity_idxs, out);
+    return ECG_OK;
+}
+
+int RSCode::partial_decoding_matrix(std::vector<int> lsi, std::vector<int> si, std::vector<int> fi,
+                                    std::vector<int>& out) {  // rs.cpp:55-66
+    if ((int)si.size() > k || !ids_in_range(si, k + m) || !ids_in_range(fi, k + m)) return ECG_EINVAL;
+    std::vector<int> f = full_matrix();
+    partial_decoding_matrix_(k, f.data(), lsi, si, fi, out);
+    return ECG_OK;
+}
+
+std::string RSCode::self_information() const {
+    return "RS(" + std::to_string(k) + "," + std::to_string(m) + ")";
+}
+
+void EnlargedRSCode::init_coding_parameters(const CodingParameters& cp) {  // rs.cpp:282-288
+    k = cp.k;
+    m = cp.m;
+    x = cp.x;
+    seri_num = cp.seri_num;
+}
+
+int EnlargedRSCode::make_encoding_matrix(int* final_matrix) {  // rs.cpp:290-305
+    if (seri_num >= x) return ECG_OK;  // "Invalid argurments!": the caller's zeros stay
+    std::vector<int> big = reed_sol_vandermonde_coding_matrix(x * k, m);
+    if (big.empty()) return ECG_EINVAL;
+    for (int i = 0; i < m; i++)
+        memcpy(&final_matrix[(size_t)i * k], &big[(size_t)i * k * x + (size_t)seri_num * k], (size_t)k * sizeof(int));
+    return ECG_OK;
+}
+
+std::string EnlargedRSCode::self_information() const {
+    return "EnlargedRS(" + std::to_string(k) + "," + std::to_string(m) + "|" + std::to_string(x) + "," +
+           std::to_string(seri_num) + ")";
+}
+
+// ================================================================================== LRC base
+
+void LocallyRepairableCode::init_coding_parameters(const CodingParameters& cp) {  // lrc.cpp:5-12
+    k = cp.k;
+    l = cp.l;
+    g = cp.g;
+    m = l + g;
+    local_or_column = cp.local_or_column != 0;
+}
+
+void LocallyRepairableCode::get_coding_parameters(CodingParameters& cp) const {  // lrc.cpp:14-21
+    cp.k = k;
+    cp.l = l;
+    cp.g = g;
+    cp.m = m;
+    cp.local_or_column = local_or_column;
+}
+
+int LocallyRepairableCode::encode(char** data_ptrs, char** coding_ptrs, int block_size) {  // lrc.cpp:23-30
+    std::vector<int> M((size_t)(g + l) * k, 0);
+    int rc = make_encoding_matrix(M.data());
+    if (rc != ECG_OK) return rc;
+    return run_encode(k, g + l, M.data(), data_ptrs, coding_ptrs, block_size);
+}
+
+// lrc.cpp:32-42: the LRC local path carries group_id in erasures[failed_num] and overwrites it with -1.
+int LocallyRepairableCode::decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures,
+                                  int failed_num) {
+    if (local_or_column) {
+        const int group_id = erasures[failed_num];
+        erasures[failed_num] = -1;
+        return decode_local(data_ptrs, coding_ptrs, block_size, erasures, failed_num, group_id);
+    }
+    return decode_global(data_ptrs, coding_ptrs, block_size, erasures, failed_num);
+}
+
+int LocallyRepairableCode::decode_global(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures,
+                                         int failed_num) {  // lrc.cpp:44-56
+    std::vector<int> M((size_t)(g + l) * k, 0);
+    int rc = make_encoding_matrix(M.data());
+    if (rc != ECG_OK) return rc;
+    return run_decode(k, g + l, M.data(), failed_num, erasures, data_ptrs, coding_ptrs, block_size);
+}
+
+int LocallyRepairableCode::decode_local(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures,
+                                        int failed_num, int group_id) {  // lrc.cpp:58-72
+    int min_idx = 0;
+    const int gs = get_group_size(group_id, min_idx);
+    if (gs < 1) return ECG_EINVAL;
+    std::vector<int> gm((size_t)gs, 0);
+    int rc = make_group_matrix(gm.data(), group_id, gs);
+    if (rc != ECG_OK) return rc;
+    return run_decode(gs, 1, gm.data(), failed_num, erasures, data_ptrs, coding_ptrs, block_size);
+}
+
+std::vector<int> LocallyRepairableCode::full_matrix() {  // lrc.cpp:107-110
+    std::vector<int> f((size_t)(k + g + l) * k, 0);
+    get_full_matrix(f.data(), k);
+    make_encoding_matrix(&f[(size_t)k * k]);
+    return f;
+}
+
+std::vector<int> LocallyRepairableCode::group_full_matrix(int gs, int group_id) {  // lrc.cpp:154-156
+    std::vector<int> f((size_t)(gs + 1) * gs, 0);
+    get_full_matrix(f.data(), gs);
+    make_group_matrix(&f[(size_t)gs * gs], group_id, gs);
+    return f;
+}
+
+int LocallyRepairableCode::remap_local(int idx, int gs, int min_idx) const {  // lrc.cpp:140-152,184-205
+    return idx >= k + g ? gs : idx - min_idx;
+}
+
+int LocallyRepairableCode::partial_encoding_matrix(std::vector<int> data_idxs, std::vector<int> parity_idxs,
+                                                   std::vector<int>& out) {
+    if (parity_idxs.empty()) return ECG_EINVAL;
+    if (!local_or_column) {  // lrc.cpp:103-113
+        if (!ids_in_range(data_idxs, k) || !ids_in_range(parity_idxs, k + g + l)) return ECG_EINVAL;
+        std::vector<int> f = full_matrix();
+        partial_encoding_matrix_(k, f.data(), data_idxs, parity_idxs, out);
+        return ECG_OK;
+    }
+    // lrc.cpp:128-159 (Opt_Cau_LRC: 1309-1346 through remap_local)
+    const int group_id = parity_idxs[0] - k - g;
+    int min_idx = -1;
+    const int gs = get_group_size(group_id, min_idx);
+    if (gs < 1) return ECG_EINVAL;
+    for (int& i : data_idxs) i = remap_local(i, gs, min_idx);
+    for (int& i : parity_idxs) i = remap_local(i, gs, min_idx);
+    if (!ids_in_range(data_idxs, gs) || !ids_in_range(parity_idxs, gs + 1)) return ECG_EINVAL;
+    std::vector<int> f = group_full_matrix(gs, group_id);
+    partial_encoding_matrix_(gs, f.data(), data_idxs, parity_idxs, out);
+    return ECG_OK;
+}
+
+int LocallyRepairableCode::partial_decoding_matrix(std::vector<int> lsi, std::vector<int> si, std::vector<int> fi,
+                                                   std::vector<int>& out) {
+    if (!local_or_column) {  // lrc.cpp:115-126
+        if ((int)si.size() > k || !ids_in_range(si, k + g + l) || !ids_in_range(fi, k + g + l)) return ECG_EINVAL;
+        std::vector<int> f = full_matrix();
+        partial_decoding_matrix_(k, f.data(), lsi, si, fi, out);
+        return ECG_OK;
+    }
+    // lrc.cpp:161-213 (Opt_Cau_LRC: 1348-1413 through remap_local)
+    const int gs = (int)si.size();
+    int group_id = -1, min_idx = k + g + l;
+    for (int idx : si) {
+        if (idx >= k + g) group_id = idx - k - g;
+        min_idx = std::min(min_idx, idx);
+    }
+    for (int idx : fi) {
+        if (idx >= k + g) group_id = idx - k - g;
+        min_idx = std::min(min_idx, idx);
+    }
+    for (int& i : si) i = remap_local(i, gs, min_idx);
+    for (int& i : fi) i = remap_local(i, gs, min_idx);
+    for (int& i : lsi) i = remap_local(i, gs, min_idx);
+    if (gs < 1 || !ids_in_range(si, gs + 1) || !ids_in_range(fi, gs + 1)) return ECG_EINVAL;
+    std::vector<int> f = group_full_matrix(gs, group_id);
+    partial_decoding_matrix_(gs, f.data(), lsi, si, fi, out);
+    return ECG_OK;
+}
+
+int LocallyRepairableCode::check_if_decodable(const std::vector<int>&) { return 1; }  // lrc.h:59
+
+// ---- Azure LRC (lrc.cpp:576-880)
+int Azu_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:622-644
+    std::vector<int> G = reed_sol_vandermonde_coding_matrix(k, g);
+    if (G.empty()) return ECG_EINVAL;
+    std::fill(M, M + (size_t)k * (g + l), 0);
+    std::copy(G.begin(), G.end(), M);
+    for (int i = 0; i < l; i++)
+        for (int j = 0; j < k; j++)
+            if (i * r <= j && j < (i + 1) * r) M[(size_t)(i + g) * k + j] = 1;
+    return ECG_OK;
+}
+
+int Azu_LRC::make_group_matrix(int* gm, int group_id, int size) {  // lrc.cpp:646-656
+    if (group_id >= 0 && group_id < l) {
+        const int gs = std::min(r, k - group_id * r);
+        for (int j = 0; j < gs && j < size; j++) gm[j] = 1;
+    }
+    return ECG_OK;
+}
+
+int Azu_LRC::bid2gid(int b) {  // lrc.cpp:665-676
+    if (b < k) return b / r;
+    if (b < k + g) return l;
+    return b - k - g;
+}
+
+int Azu_LRC::idxingroup(int b) {  // lrc.cpp:678-691
+    if (b < k) return b % r;
+    if (b < k + g) return b - k;
+    if (b - k - g < l - 1) return r;
+    return k % r == 0 ? r : k % r;
+}
+
+int Azu_LRC::get_group_size(int group_id, int& min_idx) {  // lrc.cpp:693-704
+    min_idx = group_id * r;
+    if (group_id < l - 1) return r;
+    if (group_id == l - 1) return k % r == 0 ? r : k % r;
+    min_idx = k;
+    return g;
+}
+
+int Azu_LRC::check_if_decodable(const std::vector<int>& failure_idxs) {  // lrc.cpp:576-620
+    std::vector<int> b2g(k, 0), fd(l, 0), slp(l, 1);
+    int sgp = g, idx = 0;
+    for (int i = 0; i < l; i++) {
+        const int gs = std::min(r, k - i * r);
+        for (int j = 0; j < gs; j++) b2g[idx++] = i;
+    }
+    for (int b : failure_idxs) {
+        if (b < k) fd[b2g[b]] += 1;
+        else if (b < k + g) sgp -= 1;
+        else slp[b - k - g] -= 1;
+    }
+    for (int i = 0; i < l; i++)
+        if (slp[i] && slp[i] <= fd[i]) {
+            fd[i] -= slp[i];
+            slp[i] = 0;
+        }
+    for (int i = 0; i < l; i++) {
+        if (sgp >= fd[i]) {
+            sgp -= fd[i];
+            fd[i] = 0;
+        } else {
+            return 0;
+        }
+    }
+    return 1;
+}
+
+std::string Azu_LRC::self_information() const {
+    return "Azure_LRC(" + std::to_string(k) + "," + std::to_string(l) + "," + std::to_string(g) + ")";
+}
+
+// L (l x (k+g)) * [I_k ; G] -> local rows (Azure+1 lrc.cpp:951-974, Optimal lrc.cpp:1183-1209)
+static std::vector<int> mix_local(const std::vector<int>& L, const std::vector<int>& G, int k, int g, int l) {
+    std::vector<int> dg((size_t)(k + g) * k, 0);
+    for (int i = 0; i < k; i++) dg[(size_t)i * k + i] = 1;
+    std::copy(G.begin(), G.end(), dg.begin() + (size_t)k * k);
+    return matrix_multiply(L.data(), dg.data(), l, k + g, k + g, k);
+}
+
+// ---- Azure LRC + 1 (lrc.cpp:881-1094)
+int Azu_LRC_1::make_encoding_matrix(int* M) {  // lrc.cpp:933-981
+    std::vector<int> G = reed_sol_vandermonde_coding_matrix(k, g);
+    if (G.empty() || l < 1) return ECG_EINVAL;
+    std::fill(M, M + (size_t)k * (g + l), 0);
+    std::copy(G.begin(), G.end(), M);
+    std::vector<int> L((size_t)l * (k + g), 0);
+    int idx = 0;
+    for (int i = 0; i < l - 1; i++)
+        for (int j = 0; j < std::min(r, k - i * r); j++) L[(size_t)i * (k + g) + idx++] = 1;
+    for (int j = 0; j < g; j++) L[(size_t)(l - 1) * (k + g) + idx++] = 1;
+    std::vector<int> mix = mix_local(L, G, k, g, l);
+    std::copy(mix.begin(), mix.end(), M + (size_t)g * k);
+    return ECG_OK;
+}
+
+int Azu_LRC_1::make_group_matrix(int* gm, int group_id, int size) {  // lrc.cpp:983-999
+    if (group_id == l - 1) {
+        for (int j = 0; j < g && j < size; j++) gm[j] = 1;
+        return ECG_OK;
+    }
+    if (group_id >= 0 && group_id < l - 1) {
+        const int gs = std::min(r, k - group_id * r);
+        for (int j = 0; j < gs && j < size; j++) gm[j] = 1;
+    }
+    return ECG_OK;
+}
+
+int Azu_LRC_1::bid2gid(int b) {  // lrc.cpp:1008-1019
+    if (b < k) return b / r;
+    if (b < k + g) return l - 1;
+    return b - k - g;
+}
+
+int Azu_LRC_1::idxingroup(int b) {  // lrc.cpp:1021-1036
+    if (b < k) return b % r;
+    if (b < k + g) return b - k;
+    if (b - k - g < l - 2) return r;
+    if (b - k - g == l - 2) return k % r == 0 ? r : k % r;
+    return g;
+}
+
+int Azu_LRC_1::get_group_size(int group_id, int& min_idx) {  // lrc.cpp:1038-1049
+    min_idx = group_id * r;
+    if (group_id < l - 2) return r;
+    if (group_id == l - 2) return k % r == 0 ? r : k % r;
+    min_idx = k;
+    return g;
+}
+
+std::string Azu_LRC_1::self_information() const {
+    return "Azure_LRC+1(" + std::to_string(k) + "," + std::to_string(l) + "," + std::to_string(g) + ")";
+}
+
+// ---- Optimal LRC (lrc.cpp:1096-1307)
+int Opt_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:1168-1215
+    std::vector<int> G = reed_sol_vandermonde_coding_matrix(k, g);
+    if (G.empty()) return ECG_EINVAL;
+    std::fill(M, M + (size_t)k * (g + l), 0);
+    std::copy(G.begin(), G.end(), M);
+    std::vector<int> L((size_t)l * (k + g), 0);
+    int idx = 0;
+    for (int i = 0; i < l; i++)
+        for (int j = 0; j < std::min(r, k + g - i * r); j++) L[(size_t)i * (k + g) + idx++] = 1;
+    std::vector<int> mix = mix_local(L, G, k, g, l);
+    std::copy(mix.begin(), mix.end(), M + (size_t)g * k);
+    return ECG_OK;
+}
+
+int Opt_LRC::make_group_matrix(int* gm, int group_id, int size) {  // lrc.cpp:1217-1227
+    if (group_id >= 0 && group_id < l) {
+        const int gs = std::min(r, k + g - group_id * r);
+        for (int j = 0; j < gs && j < size; j++) gm[j] = 1;
+    }
+    return ECG_OK;
+}
+
+int Opt_LRC::bid2gid(int b) { return b < k + g ? b / r : b - k - g; }  // lrc.cpp:1236-1245
+
+int Opt_LRC::idxingroup(int b) {  // lrc.cpp:1247-1258
+    if (b < k + g) return b % r;
+    if (b - k - g < l - 1) return r;
+    return (k + g) % r == 0 ? r : (k + g) % r;
+}
+
+int Opt_LRC::get_group_size(int group_id, int& min_idx) {  // lrc.cpp:1260-1268
+    min_idx = group_id * r;
+    if (group_id < l - 1) return r;
+    return (k + g) % r == 0 ? r : (k + g) % r;
+}
+
+std::string Opt_LRC::self_information() const {
+    return "Optimal_LRC(" + std::to_string(k) + "," + std::to_string(l) + "," + std::to_string(g) + ")";
+}
+
+// ---- Optimal Cauchy LRC (lrc.cpp:1309-1755)
+int Opt_Cau_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:1485-1518
+    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
+    std::fill(M, M + (size_t)k * (g + l), 0);
+    std::copy(C.begin(), C.begin() + (size_t)g * k, M);
+    int d = 0;
+    for (int i = 0; i < l; i++)
+        for (int j = 0; j < k; j++)
+            if (i * r <= j && j < (i + 1) * r) M[(size_t)(i + g) * k + j] = C[(size_t)g * k + d++];
+    for (int i = 0; i < l; i++)  // galois_region_xor of every global row into every local row
+        for (int j = 0; j < g; j++)
+            for (int t = 0; t < k; t++) M[(size_t)(i + g) * k + t] ^= C[(size_t)j * k + t];
+    return ECG_OK;
+}
+
+int Opt_Cau_LRC::make_group_matrix(int* gm, int group_id, int size) {  // lrc.cpp:1574-1591
+    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
+    int idx = 0;
+    for (int i = 0; i < l; i++) {
+        const int gs = std::min(r, k - i * r);
+        for (int j = 0; j < gs; j++) {
+            if (i == group_id && j < size) gm[j] = C[(size_t)g * k + idx];
+            idx++;
+        }
+        for (int j = gs; j < gs + g; j++)
+            if (i == group_id && j < size) gm[j] = 1;
+    }
+    return ECG_OK;
+}
+
+int Opt_Cau_LRC::bid2gid(int b) {  // lrc.cpp:1600-1611
+    if (b < k) return b / r;
+    if (b < k + g) return l;
+    return b - k - g;
+}
+
+int Opt_Cau_LRC::idxingroup(int b) {  // lrc.cpp:1613-1626
+    if (b < k) return b % r;
+    if (b < k + g) return b - k + r;
+    if (b - k - g < l - 1) return r + g;
+    return k % r == 0 ? r + g : k % r + g;
+}
+
+int Opt_Cau_LRC::get_group_size(int group_id, int& min_idx) {  // lrc.cpp:1628-1639
+    min_idx = group_id * r;
+    if (group_id < l - 1) return r + g;
+    if (group_id == l - 1) return (k % r == 0 ? r : k % r) + g;
+    min_idx = k;
+    return g;
+}
+
+int Opt_Cau_LRC::remap_local(int idx, int gs, int min_idx) const {  // lrc.cpp:1320-1340
+    if (idx >= k + g) return gs;
+    if (idx >= k) return gs - g + idx - k;
+    return idx - min_idx;
+}
+
+std::string Opt_Cau_LRC::self_information() const {
+    return "Optimal_Cauchy_LRC(" + std::to_string(k) + "," + std::to_string(l) + "," + std::to_string(g) + ")";
+}
+
+// ---- Uniform Cauchy LRC (lrc.cpp:2025-2310)
+int Uni_Cau_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:2097-2156
+    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
+    std::fill(M, M + (size_t)k * (g + l), 0);
+    std::copy(C.begin(), C.begin() + (size_t)g * k, M);
+    std::vector<int> L((size_t)l * k, 0);
+    int d = 0, l_idx = 0;
+    for (int i = 0; i < l && d < k; i++) {
+        const int gs = std::min(r, k + g - i * r);
+        for (int j = 0; j < gs && d < k; j++, d++) L[(size_t)i * k + d] = C[(size_t)g * k + d];
+        l_idx = i;
+    }
+    int g_idx = 0;
+    for (int i = l_idx; i < l; i++) {
+        const int gs = std::min(r, k + g - i * r);
+        const int sub = gs < r ? g - g_idx : (i + 1) * r - (k + g_idx);
+        for (int j = 0; j < sub && g_idx < g; j++, g_idx++)
+            for (int t = 0; t < k; t++) L[(size_t)i * k + t] ^= C[(size_t)g_idx * k + t];
+    }
+    std::copy(L.begin(), L.end(), M + (size_t)g * k);
+    return ECG_OK;
+}
+
+int Uni_Cau_LRC::make_group_matrix(int* gm, int group_id, int size) {  // lrc.cpp:2213-2230
+    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
+    int idx = 0;
+    for (int i = 0; i < l; i++) {
+        const int gs = std::min(r, k + g - i * r);
+        for (int j = 0; j < gs; j++) {
+            if (i == group_id && j < size) gm[j] = idx < k ? C[(size_t)g * k + idx] : 1;
+            idx++;
+        }
+    }
+    return ECG_OK;
+}
+
+int Uni_Cau_LRC::bid2gid(int b) { return b < k + g ? b / r : b - k - g; }  // lrc.cpp:2239-2248
+
+int Uni_Cau_LRC::idxingroup(int b) {  // lrc.cpp:2250-2261
+    if (b < k + g) return b % r;
+    if (b - k - g < l - 1) return r;
+    return (k + g) % r == 0 ? r : (k + g) % r;
+}
+
+int Uni_Cau_LRC::get_group_size(int group_id, int& min_idx) {  // lrc.cpp:2263-2271
+    min_idx = group_id * r;
+    if (group_id < l - 1) return r;
+    return (k + g) % r == 0 ? r : (k + g) % r;
+}
+
+std::string Uni_Cau_LRC::self_information() const {
+    return "Uniform_Cauchy_LRC(" + std::to_string(k) + "," + std::to_string(l) + "," + std::to_string(g) + ")";
+}
+
+// ================================================================================== Product codes
+
+void ProductCode::init_coding_parameters(const CodingParameters& cp) {  // pc.cpp:5-18
+    k1 = cp.k1;
+    m1 = cp.m1;
+    k2 = cp.k2;
+    m2 = cp.m2;
+    k = k1 * k2;
+    m = (k1 + m1) * (k2 + m2) - k;
+    row_code.k = k1;
+    row_code.m = m1;
+    col_code.k = k2;
+    col_code.m = m2;
+    local_or_column = cp.local_or_column != 0;
+}
+
+void ProductCode::get_coding_parameters(CodingParameters& cp) const {  // pc.cpp:20-29
+    cp.k1 = k1;
+    cp.m1 = m1;
+    cp.k2 = k2;
+    cp.m2 = m2;
+    cp.k = k;
+    cp.m = m;
+    cp.local_or_column = local_or_column;
+}
+
+// [row][col] -> id in the data (k) ++ coding (m) block space; pc.cpp:31-38, 86-108 ordering
+std::vector<std::vector<int>> ProductCode::block_map() const {
+    std::vector<std::vector<int>> bm(k2 + m2, std::vector<int>(k1 + m1, -1));
+    int di = 0, pi = 0;
+    for (int i = 0; i < k2; i++)
+        for (int j = 0; j < k1 + m1; j++) bm[i][j] = j < k1 ? di++ : k + pi++;
+    int gi = k2 * m1 + m2 * k1;
+    for (int i = k2; i < k2 + m2; i++)
+        for (int j = 0; j < k1 + m1; j++) {
+            if (j < k1) bm[i][j] = k + pi++;
+            else if (has_global()) bm[i][j] = k + gi++;
+        }
+    return bm;
+}
+
+int ProductCode::encode(char** data_ptrs, char** coding_ptrs, int block_size) {  // pc.cpp:39-76
+    Plan p;
+    for (int i = 0; i < k2; i++) {
+        std::vector<int> d(k1), c(m1);
+        for (int j = 0; j < k1; j++) d[j] = i * k1 + j;
+        for (int j = 0; j < m1; j++) c[j] = k + i * m1 + j;
+        int rc = rowc().plan_encode(p, d, c);
+        if (rc != ECG_OK) return rc;
+    }
+    for (int i = 0; i < k1 + m1; i++) {
+        std::vector<int> d(k2), c(m2);
+        for (int j = 0; j < k2; j++) d[j] = i < k1 ? j * k1 + i : k + j * m1 + i - k1;
+        for (int j = 0; j < m2; j++) c[j] = i < k1 ? k + k2 * m1 + j * k1 + i : k + k2 * m1 + k1 * m2 + j * m1 + i - k1;
+        int rc = colc().plan_encode(p, d, c);
+        if (rc != ECG_OK) return rc;
+    }
+    return run(p, data_ptrs, k, coding_ptrs, m, block_size);
+}
+
+// Iterative control flow of pc.cpp:79-195 (and HVPC pc.cpp:921-1029 with ncols = k1, nrows = k2).
+int ProductCode::plan_iterative_decode(Plan& p, int* erasures, int failed_num, int ncols, int nrows) {
+    const std::vector<std::vector<int>> bm = block_map();
+    std::vector<std::vector<int>> fmap(k2 + m2, std::vector<int>(k1 + m1, 0));
+    std::vector<int> frc(k2 + m2, 0), fcc(k1 + m1, 0);
+    for (int i = 0; i < failed_num; i++) {
+        int r = -1, c = -1;
+        bid2rowcol(erasures[i], r, c);
+        if (r < 0 || r >= k2 + m2 || c < 0 || c >= k1 + m1) return ECG_EINVAL;
+        fmap[r][c] = 1;
+        frc[r]++;
+        fcc[c]++;
+    }
+    while (failed_num > 0) {
+        for (int i = 0; i < ncols; i++) {
+            if (fcc[i] > 0 && fcc[i] <= m2) {
+                std::vector<int> er, d(k2), c(m2);
+                for (int jj = 0; jj < k2; jj++) {
+                    if (fmap[jj][i]) er.push_back(jj);
+                    d[jj] = bm[jj][i];
+                }
+                for (int jj = 0; jj < m2; jj++) {
+                    if (fmap[jj + k2][i]) er.push_back(jj + k2);
+                    c[jj] = bm[jj + k2][i];
+                }
+                er.push_back(-1);
+                (void)colc().plan_decode(p, d, c, er.data(), fcc[i]);  // failure: "[Decode] Failed!", continue
+                for (int jj = 0; jj < k2 + m2; jj++)
+                    if (fmap[jj][i]) {
+                        fmap[jj][i] = 0;
+                        failed_num--;
+                        frc[jj]--;
+                        fcc[i]--;
+                    }
+            }
+        }
+        if (failed_num == 0) break;
+        int max_row = -1;
+        for (int i = 0; i < nrows; i++) {
+            if (frc[i] > 0 && frc[i] <= m1) {
+                max_row = i;
+                std::vector<int> er, d(k1), c(m1);
+                for (int jj = 0; jj < k1; jj++) {
+                    if (fmap[i][jj]) er.push_back(jj);
+                    d[jj] = bm[i][jj];
+                }
+                for (int jj = 0; jj < m1; jj++) {
+                    if (fmap[i][jj + k1]) er.push_back(jj + k1);
+                    c[jj] = bm[i][jj + k1];
+                }
+                er.push_back(-1);
+                (void)rowc().plan_decode(p, d, c, er.data(), frc[i]);
+                for (int jj = 0; jj < k1 + m1; jj++)
+                    if (fmap[i][jj]) {
+                        fmap[i][jj] = 0;
+                        failed_num--;
+                        frc[i]--;
+                        fcc[jj]--;
+                    }
+            }
+        }
+        if (max_row == -1) return ECG_EUNDECODABLE;  // "Undecodable!!" (work planned so far still runs)
+    }
+    return ECG_OK;
+}
+
+int ProductCode::decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) {
+    Plan p;
+    const int status = plan_iterative_decode(p, erasures, failed_num, k1 + m1, k2 + m2);
+    if (status == ECG_EINVAL) return status;
+    int rc = run(p, data_ptrs, k, coding_ptrs, m, block_size);
+    return rc != ECG_OK ? rc : status;
+}
+
+int ProductCode::check_if_decodable(const std::vector<int>& failure_idxs) {  // pc.cpp:198-255
+    int failed_num = (int)failure_idxs.size();
+    std::vector<std::vector<int>> fmap(k2 + m2, std::vector<int>(k1 + m1, 0));
+    std::vector<int> frc(k2 + m2, 0), fcc(k1 + m1, 0);
+    for (int b : failure_idxs) {
+        int r, c;
+        bid2rowcol(b, r, c);
+        if (r < 0 || r >= k2 + m2 || c < 0 || c >= k1 + m1) return ECG_EINVAL;
+        fmap[r][c] = 1;
+        frc[r]++;
+        fcc[c]++;
+    }
+    const int ncols = has_global() ? k1 + m1 : k1, nrows = has_global() ? k2 + m2 : k2;
+    while (failed_num > 0) {
+        for (int i = 0; i < ncols; i++)
+            if (fcc[i] > 0 && fcc[i] <= m2)
+                for (int jj = 0; jj < k2 + m2; jj++)
+                    if (fmap[jj][i]) {
+                        fmap[jj][i] = 0;
+                        failed_num--;
+                        frc[jj]--;
+                        fcc[i]--;
+                    }
+        if (failed_num == 0) break;
+        int max_row = -1;
+        for (int i = 0; i < nrows; i++)
+            if (frc[i] > 0 && frc[i] <= m1) {
+                max_row = i;
+                for (int jj = 0; jj < k1 + m1; jj++)
+                    if (fmap[i][jj]) {
+                        fmap[i][jj] = 0;
+                        failed_num--;
+                        frc[i]--;
+                        fcc[jj]--;
+                    }
+            }
+        if (max_row == -1) return 0;
+    }
+    return 1;
+}
+
+int ProductCode::partial_encoding_matrix(std::vector<int> data_idxs, std::vector<int> parity_idxs,
+                                         std::vector<int>& out) {  // pc.cpp:257-288
+    int r, c;
+    for (int& i : data_idxs) {
+        bid2rowcol(i, r, c);
+        i = local_or_column ? r : c;
+    }
+    for (int& i : parity_idxs) {
+        bid2rowcol(i, r, c);
+        i = local_or_column ? r : c;
+    }
+    RSCode& code = local_or_column ? partial_col() : partial_row();
+    return code.partial_encoding_matrix(data_idxs, parity_idxs, out);
+}
+
+int ProductCode::partial_decoding_matrix(std::vector<int> lsi, std::vector<int> si, std::vector<int> fi,
+                                         std::vector<int>& out) {  // pc.cpp:290-324
+    int r, c;
+    for (std::vector<int>* v : {&lsi, &si, &fi})
+        for (int& i : *v) {
+            bid2rowcol(i, r, c);
+            i = local_or_column ? r : c;
+        }
+    RSCode& code = local_or_column ? partial_col() : partial_row();
+    return code.partial_decoding_matrix(lsi, si, fi, out);
+}
+
+int ProductCode::rowcol2bid(int row, int col) const {  // pc.cpp:326-340
+    if (row < k2 && col < k1) return row * k1 + col;
+    if (row < k2) return k1 * k2 + row * m1 + (col - k1);
+    if (col < k1) return (k1 + m1) * k2 + (row - k2) * k1 + col;
+    return (k1 + m1) * k2 + k1 * m2 + (row - k2) * m1 + (col - k1);
+}
+
+void ProductCode::bid2rowcol(int bid, int& row, int& col) const {  // pc.cpp:342-359
+    if (bid < k1 * k2) {
+        row = bid / k1;
+        col = bid % k1;
+    } else if (bid < (k1 + m1) * k2) {
+        const int t = bid - k1 * k2;
+        row = t / m1;
+        col = t % m1 + k1;
+    } else if (bid < (k1 + m1) * k2 + k1 * m2) {
+        const int t = bid - (k1 + m1) * k2;
+        row = t / k1 + k2;
+        col = t % k1;
+    } else {
+        const int t = bid - (k1 + m1) * k2 - k1 * m2;
+        row = t / m1 + k2;
+        col = t % m1 + k1;
+    }
+}
+
+int ProductCode::oldbid2newbid_for_merge(int old_block_id, int x, int seri_num, bool vertical) {  // pc.cpp:361-376
+    int row = -1, col = -1;
+    bid2rowcol(old_block_id, row, col);
+    if (vertical) {
+        row += seri_num * k2;
+        ProductCode pc(k1, m1, x * k2, m2);
+        return pc.rowcol2bid(row, col);
+    }
+    col += seri_num * k1;
+    ProductCode pc(x * k1, m1, k2, m2);
+    return pc.rowcol2bid(row, col);
+}
+
+std::string ProductCode::self_information() const {
+    return "PC(" + std::to_string(k1) + "," + std::to_string(m1) + "," + std::to_string(k2) + "," +
+           std::to_string(m2) + ")";
+}
+
+void HPC::init_coding_parameters(const CodingParameters& cp) {  // pc.cpp:553-574
+    ProductCode::init_coding_parameters(cp);
+    e_row_code.k = cp.k1;
+    e_row_code.m = cp.m1;
+    e_row_code.x = cp.x;
+    e_row_code.seri_num = cp.seri_num;
+    e_col_code.k = cp.k2;
+    e_col_code.m = cp.m2;
+    e_col_code.x = cp.x;
+    e_col_code.seri_num = cp.seri_num;
+}
+
+int HPC::oldbid2newbid_for_merge(int old_block_id, int, int, bool vertical) {  // pc.cpp:838-856
+    int row = -1, col = -1;
+    bid2rowcol(old_block_id, row, col);
+    if (vertical) {
+        row += e_col_code.seri_num * k2;
+        ProductCode pc(k1, m1, e_col_code.x * k2, m2);
+        return pc.rowcol2bid(row, col);
+    }
+    col += e_row_code.seri_num * k1;
+    ProductCode pc(e_row_code.x * k1, m1, k2, m2);
+    return pc.rowcol2bid(row, col);
+}
+
+std::string HPC::self_information() const {
+    return "HPC(" + std::to_string(k1) + "," + std::to_string(m1) + "," + std::to_string(k2) + "," +
+           std::to_string(m2) + "|" + std::to_string(e_col_code.x) + "," + std::to_string(e_col_code.seri_num) + ")";
+}
+
+void HVPC::init_coding_parameters(const CodingParameters& cp) {  // pc.cpp:869-882
+    ProductCode::init_coding_parameters(cp);
+    m = k1 * m2 + k2 * m1;
+}
+
+int HVPC::encode(char** data_ptrs, char** coding_ptrs, int block_size) {  // pc.cpp:890-918
+    Plan p;
+    for (int i = 0; i < k2; i++) {
+        std::vector<int> d(k1), c(m1);
+        for (int j = 0; j < k1; j++) d[j] = i * k1 + j;
+        for (int j = 0; j < m1; j++) c[j] = k + i * m1 + j;
+        int rc = row_code.plan_encode(p, d, c);
+        if (rc != ECG_OK) return rc;
+    }
+    for (int i = 0; i < k1; i++) {
+        std::vector<int> d(k2), c(m2);
+        for (int j = 0; j < k2; j++) d[j] = j * k1 + i;
+        for (int j = 0; j < m2; j++) c[j] = k + k2 * m1 + j * k1 + i;
+        int rc = col_code.plan_encode(p, d, c);
+        if (rc != ECG_OK) return rc;
+    }
+    return run(p, data_ptrs, k, coding_ptrs, m, block_size);
+}
+
+int HVPC::decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) {
+    Plan p;
+    const int status = plan_iterative_decode(p, erasures, failed_num, k1, k2);
+    if (status == ECG_EINVAL) return status;
+    int rc = run(p, data_ptrs, k, coding_ptrs, m, block_size);
+    return rc != ECG_OK ? rc : status;
+}
+
+int HVPC::check_if_decodable(const std::vector<int>& f) { return ProductCode::check_if_decodable(f); }
+
+std::string HVPC::self_information() const {
+    return "HVPC(" + std::to_string(k1) + "," + std::to_string(m1) + "," + std::to_string(k2) + "," +
+           std::to_string(m2) + ")";
+}
+
+// ================================================================================== factory
+
+ErasureCode* ec_factory(int ec_type, const CodingParameters& cp) {  // metadata.cpp:48-77
+    switch (ec_type) {
+        case ECG_RS: return new RSCode(cp.k, cp.m);
+        case ECG_ERS: {
+            auto* ec = new EnlargedRSCode(cp.k, cp.m);
+            ec->init_coding_parameters(cp);
+            return ec;
+        }
+        case ECG_AZURE_LRC: return cp.l > 0 ? new Azu_LRC(cp.k, cp.l, cp.g) : nullptr;
+        case ECG_AZURE_LRC_1: return cp.l > 1 ? new Azu_LRC_1(cp.k, cp.l, cp.g) : nullptr;
+        case ECG_OPTIMAL_LRC: return cp.l > 0 ? new Opt_LRC(cp.k, cp.l, cp.g) : nullptr;
+        case ECG_OPTIMAL_CAUCHY_LRC: return cp.l > 0 ? new Opt_Cau_LRC(cp.k, cp.l, cp.g) : nullptr;
+        case ECG_UNIFORM_CAUCHY_LRC: return cp.l > 0 ? new Uni_Cau_LRC(cp.k, cp.l, cp.g) : nullptr;
+        case ECG_PC: return new ProductCode(cp.k1, cp.m1, cp.k2, cp.m2);
+        case ECG_HIERACHICAL_PC: {
+            auto* ec = new HPC(cp.k1, cp.m1, cp.k2, cp.m2);
+            ec->init_coding_parameters(cp);
+            return ec;
+        }
+        case ECG_HV_PC: return new HVPC(cp.k1, cp.m1, cp.k2, cp.m2);
+        default: return nullptr;
+    }
+}
+
+}  // namespace ecg

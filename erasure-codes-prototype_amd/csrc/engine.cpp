@@ -1,0 +1,350 @@
+// GF(2^8) region engine.  See engine.hpp.
+#include "engine.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+
+namespace ecg {
+
+namespace {
+
+thread_local std::string t_last_error;
+
+#define ECG_HIP(call)                                                                        \
+    do {                                                                                     \
+        hipError_t _e = (call);                                                              \
+        if (_e != hipSuccess) {                                                              \
+            set_last_error(std::string(#call) + ": " + hipGetErrorString(_e));               \
+            return ECG_EHIP;                                                                 \
+        }                                                                                    \
+    } while (0)
+
+constexpr int kMaxDevices = 64;
+std::mutex g_engines_mu;
+Engine* g_engines[kMaxDevices] = {};
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Per-thread, per-device host-tier state: a non-blocking stream and a growable device scratch.
+struct ThreadCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t* scratch = nullptr;
+    size_t cap = 0;
+    void** d_ptrs = nullptr;     // pointer tables for ops too wide for kernel arguments
+    size_t d_ptrs_cap = 0;
+    ~ThreadCtx() {
+        // Process teardown may already have destroyed the runtime; leak rather than fault.
+    }
+};
+
+thread_local ThreadCtx t_ctx[kMaxDevices];
+
+ThreadCtx& tctx(int device) { return t_ctx[device]; }
+
+}  // namespace
+
+const char* last_error_string() { return t_last_error.c_str(); }
+void set_last_error(const std::string& s) { t_last_error = s; }
+
+ProgramSet::~ProgramSet() {
+    if (d_tabs) (void)hipFree(d_tabs);
+    if (d_src) (void)hipFree(d_src);
+    if (d_dst) (void)hipFree(d_dst);
+}
+
+Engine::Engine(int device) : device_(device) {}
+
+Engine& Engine::instance() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDevices) dev = 0;
+    std::lock_guard<std::mutex> lk(g_engines_mu);
+    if (!g_engines[dev]) g_engines[dev] = new Engine(dev);  // lives for the process
+    return *g_engines[dev];
+}
+
+hipStream_t Engine::thread_stream() {
+    ThreadCtx& c = tctx(device_);
+    if (!c.stream) {
+        if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) c.stream = nullptr;
+        c.device = device_;
+    }
+    return c.stream;
+}
+
+size_t Engine::cache_size() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return cache_.size();
+}
+
+std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& progs, int* status) {
+    *status = ECG_OK;
+    if (progs.empty()) {
+        *status = ECG_EINVAL;
+        return nullptr;
+    }
+    const int k = progs[0].k_in(), m = progs[0].m_out();
+    if (k < 1 || m < 1) {
+        *status = ECG_EINVAL;
+        return nullptr;
+    }
+    std::string key;
+    key.reserve(16 + progs.size() * (size_t)(k * m + 4 * (k + m)));
+    auto put = [&](const void* p, size_t n) { key.append((const char*)p, n); };
+    const int np = (int)progs.size();
+    put(&k, 4);
+    put(&m, 4);
+    put(&np, 4);
+    bool binary = true;
+    for (const LinearOp& op : progs) {
+        if (op.k_in() != k || op.m_out() != m || op.coef.size() != (size_t)k * m) {
+            *status = ECG_EINVAL;
+            return nullptr;
+        }
+        put(op.coef.data(), op.coef.size());
+        put(op.src_ids.data(), op.src_ids.size() * 4);
+        put(op.dst_ids.data(), op.dst_ids.size() * 4);
+        binary &= op_is_binary(op);
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = cache_.find(key);
+        if (it != cache_.end()) return it->second;
+    }
+    auto ps = std::make_shared<ProgramSet>();
+    ps->nprog = np;
+    ps->k = k;
+    ps->m = m;
+    ps->MT = std::min(m, kMaxMT);
+    ps->rtiles = (m + ps->MT - 1) / ps->MT;
+    ps->binary = binary;
+    const size_t per_prog = (size_t)ps->rtiles * k * ps->MT;
+    std::vector<CoefTab> tabs(per_prog * np);
+    std::vector<int> src((size_t)np * k), dst((size_t)np * m);
+    for (int pi = 0; pi < np; pi++) {
+        const LinearOp& op = progs[pi];
+        for (int rt = 0; rt < ps->rtiles; rt++)
+            for (int j = 0; j < k; j++)
+                for (int p = 0; p < ps->MT; p++) {
+                    const int row = rt * ps->MT + p;
+                    const int c = row < m ? op.coef[(size_t)row * k + j] : 0;
+                    make_coef_tab(c, &tabs[pi * per_prog + ((size_t)rt * k + j) * ps->MT + p]);
+                }
+        std::copy(op.src_ids.begin(), op.src_ids.end(), src.begin() + (size_t)pi * k);
+        std::copy(op.dst_ids.begin(), op.dst_ids.end(), dst.begin() + (size_t)pi * m);
+    }
+    auto fail = [&](hipError_t e, const char* what) {
+        set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+        *status = ECG_EHIP;
+        return nullptr;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&ps->d_tabs, tabs.size() * sizeof(CoefTab))) != hipSuccess) return fail(e, "hipMalloc(tabs)");
+    if ((e = hipMalloc(&ps->d_src, src.size() * sizeof(int))) != hipSuccess) return fail(e, "hipMalloc(src)");
+    if ((e = hipMalloc(&ps->d_dst, dst.size() * sizeof(int))) != hipSuccess) return fail(e, "hipMalloc(dst)");
+    if ((e = hipMemcpy(ps->d_tabs, tabs.data(), tabs.size() * sizeof(CoefTab), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e, "hipMemcpy(tabs)");
+    if ((e = hipMemcpy(ps->d_src, src.data(), src.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e, "hipMemcpy(src)");
+    if ((e = hipMemcpy(ps->d_dst, dst.data(), dst.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e, "hipMemcpy(dst)");
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = cache_.find(key);
+    if (it != cache_.end()) return it->second;  // another thread won the race
+    cache_.emplace(std::move(key), ps);
+    return ps;
+}
+
+// One op over block pointers (device addresses), any k_in / m_out.
+int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st) {
+    if (op.m_out() == 0 || B == 0) return ECG_OK;
+    if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
+        for (int d : op.dst_ids) ECG_HIP(hipMemsetAsync(blocks[d], 0, (size_t)B, st));
+        return ECG_OK;
+    }
+    if (op.m_out() > kInlineDst) {  // split the outputs; every row reads the same inputs
+        for (int r0 = 0; r0 < op.m_out(); r0 += kInlineDst) {
+            LinearOp part;
+            part.src_ids = op.src_ids;
+            const int r1 = std::min(op.m_out(), r0 + kInlineDst);
+            part.dst_ids.assign(op.dst_ids.begin() + r0, op.dst_ids.begin() + r1);
+            part.coef.assign(op.coef.begin() + (size_t)r0 * op.k_in(), op.coef.begin() + (size_t)r1 * op.k_in());
+            int rc = launch_one(part, blocks, B, st);
+            if (rc != ECG_OK) return rc;
+        }
+        return ECG_OK;
+    }
+    int status = ECG_OK;
+    std::shared_ptr<ProgramSet> ps = program_set({op}, &status);
+    if (!ps) return status;
+    GfLaunch a;
+    memset(&a, 0, sizeof(a));
+    a.tabs = ps->d_tabs;
+    a.src_ids = ps->d_src;
+    a.dst_ids = ps->d_dst;
+    a.B = B;
+    a.k = ps->k;
+    a.m = ps->m;
+    a.S = 1;
+    a.MT = ps->MT;
+    a.rtiles = ps->rtiles;
+    a.binary = ps->binary ? 1 : 0;
+    bool vec_ok = true;
+    for (int d : op.dst_ids) vec_ok &= aligned16(blocks[d]);
+    for (int s : op.src_ids) vec_ok &= aligned16(blocks[s]);
+    if (op.k_in() <= kInlineSrc) {
+        for (int j = 0; j < op.k_in(); j++) a.isrc[j] = blocks[op.src_ids[j]];
+        for (int p = 0; p < op.m_out(); p++) a.idst[p] = blocks[op.dst_ids[p]];
+        ECG_HIP(launch_gf(a, GF_MODE_INLINE, vec_ok, st));
+        return ECG_OK;
+    }
+    // Wide op: device pointer tables in per-thread scratch (synchronised before reuse).
+    ThreadCtx& c = tctx(device_);
+    const size_t need = (size_t)(op.k_in() + op.m_out());
+    ECG_HIP(hipStreamSynchronize(st));
+    if (c.d_ptrs_cap < need) {
+        if (c.d_ptrs) (void)hipFree(c.d_ptrs);
+        c.d_ptrs = nullptr;
+        c.d_ptrs_cap = 0;
+        ECG_HIP(hipMalloc(&c.d_ptrs, need * sizeof(void*)));
+        c.d_ptrs_cap = need;
+    }
+    std::vector<void*> h(need);
+    for (int j = 0; j < op.k_in(); j++) h[j] = blocks[op.src_ids[j]];
+    for (int p = 0; p < op.m_out(); p++) h[op.k_in() + p] = blocks[op.dst_ids[p]];
+    ECG_HIP(hipMemcpyAsync(c.d_ptrs, h.data(), need * sizeof(void*), hipMemcpyHostToDevice, st));
+    a.src_ptrs = (const uint8_t* const*)c.d_ptrs;
+    a.dst_ptrs = (uint8_t* const*)(c.d_ptrs + op.k_in());
+    ECG_HIP(launch_gf(a, GF_MODE_PTRS, vec_ok, st));
+    ECG_HIP(hipStreamSynchronize(st));  // h[] and the table must outlive the launch
+    return ECG_OK;
+}
+
+int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B,
+                       hipStream_t st) {
+    if (B < 0) return ECG_EINVAL;
+    for (const LinearOp& op : ops) {
+        for (int id : op.src_ids)
+            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+        for (int id : op.dst_ids)
+            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+    }
+    for (const LinearOp& op : ops) {
+        int rc = launch_one(op, blocks, B, st);
+        if (rc != ECG_OK) return rc;
+    }
+    return ECG_OK;
+}
+
+int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B) {
+    if (B < 0) return ECG_EINVAL;
+    if (ops.empty() || B == 0) return ECG_OK;
+    hipStream_t st = thread_stream();
+    if (!st) return ECG_EHIP;
+    // Slots for every referenced block.
+    std::vector<int> slot(nblocks, -1);
+    int nslots = 0;
+    for (const LinearOp& op : ops) {
+        for (int id : op.src_ids) {
+            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+            if (slot[id] < 0) slot[id] = nslots++;
+        }
+        for (int id : op.dst_ids) {
+            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+            if (slot[id] < 0) slot[id] = nslots++;
+        }
+    }
+    const size_t pitch = ((size_t)B + 255) & ~(size_t)255;
+    ThreadCtx& c = tctx(device_);
+    if (c.cap < pitch * nslots) {
+        ECG_HIP(hipStreamSynchronize(st));
+        if (c.scratch) (void)hipFree(c.scratch);
+        c.scratch = nullptr;
+        c.cap = 0;
+        ECG_HIP(hipMalloc(&c.scratch, pitch * nslots));
+        c.cap = pitch * nslots;
+    }
+    std::vector<uint8_t*> dev(nblocks, nullptr);
+    for (int id = 0; id < nblocks; id++)
+        if (slot[id] >= 0) dev[id] = c.scratch + (size_t)slot[id] * pitch;
+    std::vector<char> resident(nblocks, 0), written(nblocks, 0);
+    for (const LinearOp& op : ops) {
+        for (int id : op.src_ids) {
+            if (!resident[id]) {
+                ECG_HIP(hipMemcpyAsync(dev[id], blocks[id], (size_t)B, hipMemcpyHostToDevice, st));
+                resident[id] = 1;
+            }
+        }
+        int rc = launch_one(op, dev.data(), B, st);
+        if (rc != ECG_OK) {
+            (void)hipStreamSynchronize(st);
+            return rc;
+        }
+        for (int id : op.dst_ids) resident[id] = written[id] = 1;
+    }
+    for (int id = 0; id < nblocks; id++)
+        if (written[id]) ECG_HIP(hipMemcpyAsync(blocks[id], dev[id], (size_t)B, hipMemcpyDeviceToHost, st));
+    ECG_HIP(hipStreamSynchronize(st));
+    return ECG_OK;
+}
+
+int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of_stripe, int S,
+                        const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
+                        long long out_sstride, long long out_bstride, long long B, hipStream_t st) {
+    if (S < 1 || B < 0 || !in_base || !out_base) return ECG_EINVAL;
+    if (progs.size() > 1 && !d_prog_of_stripe) return ECG_EINVAL;
+    int status = ECG_OK;
+    std::shared_ptr<ProgramSet> ps = program_set(progs, &status);
+    if (!ps) return status;
+    GfLaunch a;
+    memset(&a, 0, sizeof(a));
+    a.tabs = ps->d_tabs;
+    a.src_ids = ps->d_src;
+    a.dst_ids = ps->d_dst;
+    a.prog_of_stripe = progs.size() > 1 ? d_prog_of_stripe : nullptr;
+    a.in_base = (const uint8_t*)in_base;
+    a.out_base = (uint8_t*)out_base;
+    a.in_sstride = in_sstride;
+    a.in_bstride = in_bstride;
+    a.out_sstride = out_sstride;
+    a.out_bstride = out_bstride;
+    a.B = B;
+    a.k = ps->k;
+    a.m = ps->m;
+    a.S = S;
+    a.MT = ps->MT;
+    a.rtiles = ps->rtiles;
+    a.binary = ps->binary ? 1 : 0;
+    const bool vec_ok = aligned16(in_base) && aligned16(out_base) && (in_sstride % 16 == 0) &&
+                        (in_bstride % 16 == 0) && (out_sstride % 16 == 0) && (out_bstride % 16 == 0);
+    ECG_HIP(launch_gf(a, GF_MODE_STRIDED, vec_ok, st));
+    return ECG_OK;
+}
+
+int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
+                     bool aligned, hipStream_t st) {
+    if (S < 1 || B < 0 || !d_src || !d_dst) return ECG_EINVAL;
+    int status = ECG_OK;
+    std::shared_ptr<ProgramSet> ps = program_set({prog}, &status);
+    if (!ps) return status;
+    GfLaunch a;
+    memset(&a, 0, sizeof(a));
+    a.tabs = ps->d_tabs;
+    a.src_ids = ps->d_src;
+    a.dst_ids = ps->d_dst;
+    a.src_ptrs = d_src;
+    a.dst_ptrs = d_dst;
+    a.B = B;
+    a.k = ps->k;
+    a.m = ps->m;
+    a.S = S;
+    a.MT = ps->MT;
+    a.rtiles = ps->rtiles;
+    a.binary = ps->binary ? 1 : 0;
+    ECG_HIP(launch_gf(a, GF_MODE_PTRS, aligned, st));
+    return ECG_OK;
+}
+
+}  // namespace ecg

@@ -1,0 +1,68 @@
+// GF(2^8) region engine: turns LinearOps (matrix.hpp) into HIP launches on gfx950.
+//
+// Three ways in:
+//   run_device  - block pointers are device pointers (HBM-resident), asynchronous on a stream;
+//   run_host    - block pointers are host buffers (the reference's char** of host memory): blocks are
+//                 staged into per-thread device scratch, each block copied in at most once and every
+//                 written block copied back once, then the stream is synchronised;
+//   run_strided - batches of S stripes laid out as base + stripe/block strides, each stripe running
+//                 one of a small set of programs (e.g. 14 rotating single-erasure decode patterns).
+// Coefficient tables are built on the host once per distinct program set and cached in HBM.
+// Thread-safe: the cache is mutex-protected; host-tier scratch and streams are per thread.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ecg.h"  // status codes ECG_*
+#include "gf_kernels.hpp"
+#include "matrix.hpp"
+
+namespace ecg {
+
+struct ProgramSet {
+    CoefTab* d_tabs = nullptr;
+    int* d_src = nullptr;
+    int* d_dst = nullptr;
+    int nprog = 0, k = 0, m = 0, MT = 1, rtiles = 1;
+    bool binary = false;
+    ~ProgramSet();
+};
+
+class Engine {
+public:
+    static Engine& instance();  // engine of the calling thread's current HIP device
+
+    int run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B,
+                   hipStream_t stream);
+    int run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B);
+    int run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of_stripe, int S,
+                    const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
+                    long long out_sstride, long long out_bstride, long long B, hipStream_t stream);
+    int run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
+                 bool aligned16, hipStream_t stream);
+
+    std::shared_ptr<ProgramSet> program_set(const std::vector<LinearOp>& progs, int* status);
+    hipStream_t thread_stream();  // per-thread non-blocking stream used by the host tier
+    int device() const { return device_; }
+    size_t cache_size();
+
+private:
+    explicit Engine(int device);
+    int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream);
+
+    int device_;
+    std::mutex mu_;
+    std::unordered_map<std::string, std::shared_ptr<ProgramSet>> cache_;
+};
+
+// Last HIP error seen by this thread (for diagnostics through the C ABI).
+const char* last_error_string();
+void set_last_error(const std::string& s);
+
+}  // namespace ecg

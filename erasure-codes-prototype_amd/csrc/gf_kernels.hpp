@@ -1,0 +1,73 @@
+// Device-side GF(2^8) region-product kernels for gfx950 (CDNA4) and their launch descriptors.
+//
+// One primitive covers every byte operation on the reference's hot path:
+//   out_p = XOR_j  c[p][j] * in_j        (bytewise, GF(2^8) / 0x11d)
+// jerasure_matrix_encode (a1), the dot products of jerasure_matrix_decode (a3, composed on the host
+// into one matrix), perform_addition (a8, all-ones rows), partial encode / partial decode (a9/a10,
+// sub-matrices) and galois_region_xor (a7, a 1x2 all-ones product) are all instances.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ecg {
+
+// Per-coefficient multiply tables for v_perm_b32 (one 32-byte record, loaded into SGPRs).
+// A byte b is split into bit fields b[2:0], b[5:3], b[7:6]; c*b = T0[b&7] ^ T1[(b>>3)&7] ^ T2[b>>6]
+// (GF multiplication by a constant is linear over GF(2)).  T0/T1 have 8 one-byte entries (two dwords
+// each, the v_perm 8-byte pool), T2 has 4 (one dword).
+struct alignas(32) CoefTab {
+    uint32_t t0lo, t0hi;  // c * e        for e = 0..7
+    uint32_t t1lo, t1hi;  // c * (e << 3)
+    uint32_t t2;          // c * (e << 6) for e = 0..3
+    uint32_t mask;        // BINARY flavour: 0xffffffff if c == 1, 0 if c == 0
+    uint32_t pad0, pad1;
+};
+
+enum GfMode : int {
+    GF_MODE_INLINE = 0,   // S == 1, pointers carried in the kernel arguments
+    GF_MODE_PTRS = 1,     // device pointer tables src_ptrs[S][k], dst_ptrs[S][m]
+    GF_MODE_STRIDED = 2,  // base + stripe/block strides + per-program block ids
+};
+
+constexpr int kInlineSrc = 128;
+constexpr int kInlineDst = 32;
+constexpr int kMaxMT = 8;       // output rows per row tile
+constexpr int kThreads = 256;   // 4 waves of 64
+
+struct GfLaunch {
+    // programs: [nprog][rtiles][k][MT] tables, [nprog][k] src ids, [nprog][m] dst ids
+    const CoefTab* tabs;
+    const int* src_ids;
+    const int* dst_ids;
+    const int* prog_of_stripe;   // [S] or nullptr (program 0 for every stripe)
+    // GF_MODE_STRIDED
+    const uint8_t* in_base;
+    uint8_t* out_base;
+    long long in_sstride, in_bstride, out_sstride, out_bstride;
+    // GF_MODE_PTRS
+    const uint8_t* const* src_ptrs;
+    uint8_t* const* dst_ptrs;
+    // GF_MODE_INLINE
+    const uint8_t* isrc[kInlineSrc];
+    uint8_t* idst[kInlineDst];
+    long long B;         // block size in bytes
+    long long off0;      // byte offset this launch starts at (tail launches)
+    int k, m, S;
+    int MT, rtiles;
+    int binary;          // every coefficient is 0 or 1 -> BINARY kernel flavour
+    int wg_per_stripe;
+    int cols_per_wg;     // 16-byte columns per workgroup (vector path) / bytes per workgroup (byte path)
+};
+
+// Launch the region product over bytes [0, B) of every stripe.  `vec_ok` = every block pointer is
+// 16-byte aligned (the host checks); otherwise the byte path covers everything.  Returns a hipError_t.
+hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t stream);
+
+// Deterministic synthetic bytes: 8-byte word w = splitmix64(seed + (word_offset + w) * golden).
+hipError_t launch_fill_splitmix(void* dst, long long nbytes, unsigned long long seed,
+                                unsigned long long word_offset, hipStream_t stream);
+
+// Host-side table construction for coefficient c (product GF arithmetic, gf256.hpp).
+void make_coef_tab(int c, CoefTab* out);
+
+}  // namespace ecg

@@ -1,0 +1,155 @@
+/*
+ * ecg.h — C ABI of the MI355X (gfx950) erasure-coding engine (libecg.so).
+ *
+ * Drop-in boundary for hhlgt/erasure-codes-prototype's hot path.  Three tiers:
+ *
+ *  1. Jerasure-compatible tier — the exact C API the reference links (project/CmakeLists.txt:116-134,
+ *     "Jerasure gf_complete"), same arguments and semantics, w = 8 only.  Region arguments are HOST
+ *     pointers (char** of B-byte buffers, as the proxy passes them: proxy.cpp:335-346); the bytes are
+ *     staged through HBM and computed by the HIP kernels.  The reference's src/ec/{rs,lrc,pc,erasure_code}.cpp can be
+ *     relinked against these symbols unchanged (INTEGRATION.md shows the shim header).
+ *  2. Device / batched tier — the same operations over HBM-resident blocks, asynchronous on a HIP
+ *     stream, and batches of S stripes in one launch (what bench.py drives).
+ *  3. ErasureCode facade — handles mirroring the reference's ErasureCode class hierarchy
+ *     (project/include/ec/erasure_code.h:60-129) as built by ec_factory (project/src/metadata.cpp:48-77):
+ *     RS, EnlargedRS, the five LRCs and the three product codes, with encode / decode /
+ *     encode_partial_blocks_for_{encoding,decoding} / perform_addition.
+ *
+ * Status codes: where the reference function returns void, the ABI returns int (0 = done).  The
+ * reference prints and returns on bad input ("[Decode] Undecodable!" rs.cpp:30-33, "invalid! %d mod %d"
+ * erasure_code.cpp:73-76); the ABI returns the matching negative code instead and never exits.
+ * Thread-safety: every entry point may be called concurrently from different threads (the proxy runs
+ * EC calls on detached threads, proxy.cpp:416-419); the only shared state is a mutex-protected
+ * coefficient-table cache.
+ */
+#ifndef ECG_H
+#define ECG_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECG_OK 0
+#define ECG_EUNDECODABLE (-1) /* jerasure_matrix_decode returns -1; reference prints "[Decode] Failed!" */
+#define ECG_EINVAL (-2)       /* bad arguments (w != 8, k/m out of range, block_num % parity_num != 0) */
+#define ECG_EHIP (-3)         /* HIP runtime error; see ecg_last_error() */
+#define ECG_EUNPINNED (-4)    /* Cauchy m == 2 needs Jerasure's cbest_8 table, not available offline */
+#define ECG_ENOMEM (-5)
+
+const char* ecg_last_error(void);  /* thread-local message for the last ECG_EHIP */
+int ecg_version(void);             /* 100 * major + minor */
+int ecg_device_count(void);
+int ecg_set_device(int device);    /* selects the HIP device for the calling thread */
+void ecg_free(void* p);            /* frees matrices returned by this library (malloc'd, like Jerasure) */
+
+/* ---------------------------------------------------------------- tier 1: Jerasure-compatible (w = 8)
+ * Replaces reed_sol_vandermonde_coding_matrix  (called rs.cpp:7,34,297; lrc.cpp:624,935,1170) */
+int* ecg_reed_sol_vandermonde_coding_matrix(int k, int m, int w);
+/* Replaces cauchy_good_general_coding_matrix   (called lrc.cpp:1487,1522,1576,2099,2160,2215).
+ * Returns NULL for m == 2 (cbest_8 path: unpinned). */
+int* ecg_cauchy_good_general_coding_matrix(int k, int m, int w);
+int* ecg_cauchy_original_coding_matrix(int k, int m, int w);
+void ecg_cauchy_improve_coding_matrix(int k, int m, int w, int* matrix);
+int ecg_cauchy_n_ones(int n, int w);
+/* Replaces jerasure_invert_matrix              (called erasure_code.cpp:128; lrc.cpp:...) */
+int ecg_jerasure_invert_matrix(int* mat, int* inv, int rows, int w);
+/* Replaces jerasure_matrix_multiply            (called erasure_code.cpp:131; lrc.cpp:969,1203,1558,2197) */
+int* ecg_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int c2, int w);
+/* Replaces galois_region_xor(src, dest, nbytes): dest ^= src (host buffers, computed on the GPU) */
+int ecg_galois_region_xor(char* src, char* dest, int nbytes);
+/* Replaces jerasure_matrix_encode              (called rs.cpp:24; lrc.cpp:28; erasure_code.cpp:90,109,147) */
+int ecg_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs, int size);
+/* Replaces jerasure_matrix_decode              (called rs.cpp:36; lrc.cpp:50,66).  0 or -1 like the library. */
+int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
+                               char** coding_ptrs, int size);
+
+/* ---------------------------------------------------------------- tier 2: device / batched
+ * All pointers below are DEVICE pointers; `stream` is a hipStream_t (NULL = default stream);
+ * calls are asynchronous.  Block pointers must be 16-byte aligned for the vector path (otherwise a
+ * byte path runs).  B is any byte count. */
+int ecg_dev_matrix_encode(int k, int m, const int* matrix, char** d_data_ptrs, char** d_coding_ptrs, long long B,
+                          void* stream);
+int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const int* erasures, char** d_data_ptrs,
+                          char** d_coding_ptrs, long long B, void* stream);
+/* Generic region product: out[dst_ids[p]] = XOR_j coef[p*k_in+j] * in[src_ids[j]] for S stripes,
+ * in block b of stripe s at in_base + s*in_sstride + b*in_bstride (likewise out). */
+int ecg_matrix_apply_batch(int k_in, int m_out, const int* coef, const int* src_ids, const int* dst_ids,
+                           const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
+                           long long out_sstride, long long out_bstride, long long B, int S, void* stream);
+/* Batched jerasure_matrix_encode: in [S] x k blocks, out [S] x m blocks (coding block i at index i). */
+int ecg_encode_batch(int k, int m, const int* matrix, const void* d_in, long long in_sstride, long long in_bstride,
+                     void* d_out, long long out_sstride, long long out_bstride, long long B, int S, void* stream);
+/* Batched jerasure_matrix_decode over stripes laid out as k+m blocks (data 0..k-1, coding k..k+m-1).
+ * `patterns`: n_patterns host erasure lists, each -1-terminated, concatenated.  d_pattern_of_stripe:
+ * device int[S] (NULL if n_patterns == 1).  Every pattern must compose to the same number of read
+ * and written blocks.  d_out == NULL: written in place into the erased blocks; otherwise written
+ * block i of a stripe's pattern (library write order) goes to d_out + s*out_sstride + i*out_bstride. */
+int ecg_decode_batch(int k, int m, const int* matrix, int row_k_ones, const int* patterns, int n_patterns,
+                     const int* d_pattern_of_stripe, void* d_stripes, long long sstride, long long bstride,
+                     void* d_out, long long out_sstride, long long out_bstride, long long B, int S, void* stream);
+/* Batched perform_addition (erasure_code.cpp:70-94): parity i of stripe s = XOR_j partial[j*parity_num+i]. */
+int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, long long in_sstride,
+                               long long in_bstride, void* d_out, long long out_sstride, long long out_bstride,
+                               long long B, int S, void* stream);
+/* Deterministic synthetic bytes (splitmix64 counter). */
+int ecg_fill_random(void* d_dst, long long nbytes, unsigned long long seed, unsigned long long word_offset,
+                    void* stream);
+
+/* ---------------------------------------------------------------- tier 3: ErasureCode facade */
+enum ecg_ectype {  /* project/include/ec/erasure_code.h:17-29 */
+    ECG_RS = 0,
+    ECG_ERS = 1,
+    ECG_AZURE_LRC = 2,
+    ECG_AZURE_LRC_1 = 3,
+    ECG_OPTIMAL_LRC = 4,
+    ECG_OPTIMAL_CAUCHY_LRC = 5,
+    ECG_UNIFORM_CAUCHY_LRC = 6,
+    ECG_PC = 7,
+    ECG_HIERACHICAL_PC = 8,
+    ECG_HV_PC = 9
+};
+
+typedef struct ecg_coding_parameters {  /* erasure_code.h:38-51 */
+    int k, m, l, g, k1, m1, k2, m2, x, seri_num;
+    int local_or_column;
+} ecg_coding_parameters;
+
+#define ECG_MEM_HOST 0   /* char** point at host buffers (reference semantics, synchronous) */
+#define ECG_MEM_DEVICE 1 /* char** point at HBM buffers, asynchronous on the handle's stream */
+
+typedef struct ecg_ec ecg_ec;
+
+ecg_ec* ecg_ec_factory(int ec_type, const ecg_coding_parameters* cp); /* metadata.cpp:48-77 */
+void ecg_ec_destroy(ecg_ec* ec);
+int ecg_ec_init_coding_parameters(ecg_ec* ec, const ecg_coding_parameters* cp);
+int ecg_ec_get_coding_parameters(ecg_ec* ec, ecg_coding_parameters* cp);
+int ecg_ec_set_memory(ecg_ec* ec, int mem, void* stream);
+int ecg_ec_set_isvertical(ecg_ec* ec, int isvertical); /* HPC::isvertical (pc.h:66) */
+int ecg_ec_k(const ecg_ec* ec);
+int ecg_ec_m(const ecg_ec* ec);
+int ecg_ec_make_encoding_matrix(ecg_ec* ec, int* final_matrix); /* m x k, where the class defines one */
+int ecg_ec_check_if_decodable(ecg_ec* ec, const int* failure_idxs, int n);
+int ecg_ec_encode(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size);
+int ecg_ec_decode(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num);
+int ecg_ec_encode_partial_blocks_for_encoding(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size,
+                                              const int* data_idxs, int n_data, const int* parity_idxs,
+                                              int n_parity);
+int ecg_ec_encode_partial_blocks_for_decoding(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size,
+                                              const int* local_survivor_idxs, int n_local,
+                                              const int* survivor_idxs, int n_survivors,
+                                              const int* failure_idxs, int n_failures);
+int ecg_ec_perform_addition(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size, int block_num,
+                            int parity_num);
+/* Planning hooks for batching: the coefficient matrix (n_out x n_in, row-major) that the facade's
+ * partial call would apply to its data_ptrs -> coding_ptrs.  Returns n_out (>= 0) or a negative code;
+ * feed the result to ecg_matrix_apply_batch. */
+int ecg_ec_partial_decoding_matrix(ecg_ec* ec, const int* local_survivor_idxs, int n_local,
+                                   const int* survivor_idxs, int n_survivors, const int* failure_idxs,
+                                   int n_failures, int* out_coef, int out_cap);
+int ecg_ec_partial_encoding_matrix(ecg_ec* ec, const int* data_idxs, int n_data, const int* parity_idxs,
+                                   int n_parity, int* out_coef, int out_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECG_H */

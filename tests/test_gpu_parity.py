@@ -1,0 +1,425 @@
+"""GPU parity: the HIP path (through libecg.so's C ABI) against the oracle on the same inputs.
+
+Bit-exact for every byte.  Small sizes are compared against the oracle directly; BASELINE.json's full
+size (RS(10,4), 1 MiB blocks, 4096 stripes) is checked through size-independent properties
+(encode -> erase -> decode round trips on device) plus oracle comparisons of sampled stripes.
+"""
+import itertools
+import json
+import os
+import random
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X (torch.cuda.is_available() is False)")
+    return torch
+
+
+def rnd(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+def same(a, b):
+    return all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+# ------------------------------------------------------------------ Jerasure-compatible tier (host buffers)
+
+@pytest.mark.parametrize("k,m", [(10, 4), (6, 4), (6, 2), (12, 4), (8, 1), (1, 1), (40, 8), (130, 3)])
+@pytest.mark.parametrize("B", [1, 15, 16, 64, 1000, 4099, 65536])
+def test_matrix_encode_host(ecg, oracle, torch_cuda, k, m, B):
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m) if k + m <= 256 else None
+    data = [rnd(B, 100 * j + B) for j in range(k)]
+    a = [np.zeros(B, np.uint8) for _ in range(m)]
+    b = [np.full(B, 0x5a, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, data, a, B)
+    ecg.jerasure_matrix_encode(k, m, M, data, b, B)
+    assert same(a, b)
+
+
+def test_matrix_encode_random_matrices(ecg, oracle, torch_cuda):
+    """Arbitrary coefficient matrices (zeros, ones, all-zero rows left untouched)."""
+    rng = random.Random(2)
+    B = 777
+    for trial in range(30):
+        k, m = rng.randint(1, 20), rng.randint(1, 12)
+        M = [rng.choice([0, 1, rng.randrange(256)]) for _ in range(k * m)]
+        if trial % 5 == 0:
+            M[:k] = [0] * k  # all-zero row: destination untouched
+        data = [rnd(B, trial * 50 + j) for j in range(k)]
+        a = [rnd(B, 999 + i) for i in range(m)]
+        b = [x.copy() for x in a]
+        oracle.jerasure_matrix_encode(k, m, M, data, a, B)
+        ecg.jerasure_matrix_encode(k, m, M, data, b, B)
+        assert same(a, b), (k, m, M)
+
+
+@pytest.mark.parametrize("k,m,row_k_ones", [(6, 4, 1), (6, 4, 0), (10, 4, 1), (4, 2, 1)])
+def test_matrix_decode_host_all_patterns(ecg, oracle, torch_cuda, k, m, row_k_ones):
+    B = 1024 + 7
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    data = [rnd(B, j) for j in range(k)]
+    coding = [np.zeros(B, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, data, coding, B)
+    stripe = data + coding
+    for f in range(1, m + 2):
+        for pat in itertools.combinations(range(k + m), f):
+            if f > 2 and k >= 10 and random.Random(hash(pat)).random() < 0.8:
+                continue
+            A = [x.copy() for x in stripe]
+            Bb = [x.copy() for x in stripe]
+            for i in pat:  # erased buffers hold garbage, not zeros
+                A[i][:] = 0xEE
+                Bb[i][:] = 0xEE
+            ra = oracle.jerasure_matrix_decode(k, m, M, row_k_ones, list(pat) + [-1], A[:k], A[k:], B)
+            rb = ecg.jerasure_matrix_decode(k, m, M, row_k_ones, list(pat) + [-1], Bb[:k], Bb[k:], B)
+            assert ra == rb, pat
+            assert same(A, Bb), pat
+            if f <= m:
+                assert ra == 0 and same(A, stripe)
+
+
+def test_matrix_decode_quirky_matrices(ecg, oracle, torch_cuda):
+    """Non-MDS / non-all-ones-row matrices: row_k_ones misuse (Appendix B.1) and singular patterns
+    must be reproduced exactly, garbage included."""
+    rng = random.Random(5)
+    B = 200
+    for trial in range(60):
+        k, m = rng.randint(2, 8), rng.randint(1, 4)
+        M = [rng.choice([0, 1, 2, rng.randrange(256)]) for _ in range(k * m)]
+        stripe = [rnd(B, trial * 20 + j) for j in range(k + m)]
+        pat = rng.sample(range(k + m), rng.randint(1, m))
+        A = [x.copy() for x in stripe]
+        Bb = [x.copy() for x in stripe]
+        rko = rng.randint(0, 1)
+        ra = oracle.jerasure_matrix_decode(k, m, M, rko, pat + [-1], A[:k], A[k:], B)
+        rb = ecg.jerasure_matrix_decode(k, m, M, rko, pat + [-1], Bb[:k], Bb[k:], B)
+        assert ra == rb and same(A, Bb), (k, m, M, pat, rko)
+
+
+def test_galois_region_xor(ecg, oracle, torch_cuda):
+    for n in (1, 17, 4096, 100003):
+        s, d = rnd(n, 1), rnd(n, 2)
+        d2 = d.copy()
+        oracle.galois_region_xor(s, d, n)
+        ecg.galois_region_xor(s, d2, n)
+        assert np.array_equal(d, d2)
+
+
+# ------------------------------------------------------------------ ErasureCode facade vs oracle classes
+
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+
+
+def test_facade_encode_matches_golden(ecg, torch_cuda):
+    B = GOLDEN["block_size"]
+    for c in GOLDEN["codes"]:
+        ec = ecg.ec_factory(c["type"], ecg.CodingParameters(**c["params"]))
+        data = [np.frombuffer(bytes.fromhex(h), np.uint8).copy() for h in c["data_hex"]]
+        coding = [np.zeros(B, np.uint8) for _ in range(ec.m)]
+        assert ec.encode(data, coding, B) == 0
+        assert [x.tobytes().hex() for x in coding] == c["coding_hex"], c["name"]
+
+
+CODES = [(c["name"], c["type"], c["params"]) for c in GOLDEN["codes"]]
+
+
+def _pair(t, params, local=False):
+    from oracle import ec_ref as E
+    import ecg as P
+    cp = dict(params, local_or_column=local)
+    o = E.ec_factory(t, E.CodingParameters(**cp))
+    p = P.ec_factory(t, P.CodingParameters(**cp))
+    o.local_or_column = local
+    p.init_coding_parameters(P.CodingParameters(**cp)) if local else None
+    if local and hasattr(o, "e_row_code"):  # HPC init also resets ERS parts
+        o.init_coding_parameters(E.CodingParameters(**cp))
+    return o, p
+
+
+@pytest.mark.parametrize("name,t,params", CODES)
+def test_facade_decode_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
+    rng = random.Random(name)
+    B = 4096 + 5
+    o, p = _pair(t, params)
+    from oracle import ec_ref as E
+    data = E.blocks(o.k, B, 77)
+    coding = E.zeros(o.m, B)
+    o.encode(data, coding, B)
+    stripe = data + coding
+    n = o.k + o.m
+    for _ in range(12):
+        pat = rng.sample(range(n), rng.randint(1, min(4, o.m)))
+        A = [x.copy() for x in stripe]
+        Bb = [x.copy() for x in stripe]
+        for i in pat:
+            A[i][:] = 0
+            Bb[i][:] = 0
+        if t in (2, 3, 4, 5, 6):  # LRC global decode: -1-terminated list
+            ea, eb = pat + [-1], pat + [-1]
+        else:
+            ea, eb = pat + [-1], pat + [-1]
+        ra = o.decode(A[:o.k], A[o.k:], B, ea, len(pat))
+        rb = p.decode(Bb[:o.k], Bb[o.k:], B, eb, len(pat))
+        assert (ra == 0) == (rb == 0), (pat, ra, rb)
+        assert same(A, Bb), pat
+
+
+@pytest.mark.parametrize("name,t,params", CODES)
+def test_facade_partials_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
+    from oracle import ec_ref as E
+    rng = random.Random(name + "p")
+    B = 1000
+    for local in (False, True):
+        o, p = _pair(t, params, local)
+        if local and t in (0, 1):
+            continue
+        data = E.blocks(o.k, B, 3)
+        coding = E.zeros(o.m, B)
+        o.encode(data, coding, B)
+        stripe = data + coding
+        k, m = o.k, o.m
+        for _ in range(6):
+            if t >= 7:  # product codes: one row (or column) of the grid
+                if not local:
+                    r = rng.randrange(o.k2)
+                    members = [o.rowcol2bid(r, c) for c in range(o.k1 + o.m1)]
+                    nd = o.k1
+                else:
+                    c = rng.randrange(o.k1)
+                    members = [o.rowcol2bid(r, c) for r in range(o.k2 + o.m2)]
+                    nd = o.k2
+                d_all, par = members[:nd], members[nd:]
+            elif local:
+                gid = rng.randrange(o.l)
+                gs, mn = o.get_group_size(gid)
+                if name.startswith("OptCauchy"):
+                    d_all = list(range(mn, mn + gs - o.g)) + list(range(k, k + o.g))
+                else:
+                    d_all = list(range(mn, mn + gs))
+                par = [k + o.g + gid]
+            else:
+                d_all, par = list(range(k)), list(range(k, k + (o.g if hasattr(o, "g") else m)))
+            cut = rng.randint(1, len(d_all) - 1) if len(d_all) > 1 else 1
+            sub = rng.sample(d_all, cut)
+            outs_a, outs_b = E.zeros(len(par), B), E.zeros(len(par), B)
+            o.encode_partial_blocks_for_encoding([stripe[i] for i in sub], outs_a, B, sub, par)
+            p.encode_partial_blocks_for_encoding([stripe[i] for i in sub], outs_b, B, sub, par)
+            assert same(outs_a, outs_b), ("enc", local, sub, par)
+            # partial decoding: lose one member, survivors = the rest (exactly k' of them)
+            group = d_all + par
+            lost = rng.choice(group)
+            surv = [i for i in group if i != lost][:len(d_all)]
+            lsub = rng.sample(surv, rng.randint(1, len(surv)))
+            da, db = E.zeros(1, B), E.zeros(1, B)
+            o.encode_partial_blocks_for_decoding([stripe[i] for i in lsub], da, B, lsub, surv, [lost])
+            p.encode_partial_blocks_for_decoding([stripe[i] for i in lsub], db, B, lsub, surv, [lost])
+            assert same(da, db), ("dec", local, lsub, surv, lost)
+
+
+def test_perform_addition(ecg, oracle, torch_cuda):
+    from oracle import ec_ref as E
+    o = E.RSCode(4, 2)
+    p = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=4, m=2))
+    for n, par, B in [(2, 1, 1 << 20), (6, 2, 1001), (12, 4, 64), (9, 3, 16)]:
+        parts = [rnd(B, 10 * i + n) for i in range(n)]
+        a, b = E.zeros(par, B), E.zeros(par, B)
+        o.perform_addition(parts, a, B, n, par)
+        assert p.perform_addition(parts, b, B, n, par) == 0
+        assert same(a, b)
+
+
+def test_lrc_local_decode_side_channel(ecg, oracle, torch_cuda):
+    """LRC local decode: group_id rides in erasures[failed_num] and is overwritten with -1 (lrc.cpp:35-38)."""
+    from oracle import ec_ref as E
+    B = 4096
+    o, p = _pair(2, dict(k=12, l=2, g=2), local=True)
+    data = E.blocks(12, B, 1)
+    coding = E.zeros(4, B)
+    o.encode(data, coding, B)
+    group = data[6:12] + [coding[3]]  # group 1: blocks 6..11, local parity 15
+    for lost in range(6):
+        A = [x.copy() for x in group]
+        A[lost][:] = 0
+        er = [lost, 1]
+        assert p.decode(A[:6], A[6:], B, er, 1) == 0
+        assert er == [lost, -1]
+        assert np.array_equal(A[lost], group[lost])
+
+
+# ------------------------------------------------------------------ device tier + batches
+
+def test_device_tier_aligned_and_unaligned(ecg, oracle, torch_cuda):
+    torch = torch_cuda
+    k, m = 10, 4
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    for B, off in [(65536, 0), (4099, 0), (4096, 1), (777, 3)]:
+        host = [rnd(B, j + B) for j in range(k)]
+        dev_data = [torch.from_numpy(np.concatenate([np.zeros(off, np.uint8), h])).cuda()[off:] for h in host]
+        dev_cod = [torch.zeros(B + off, dtype=torch.uint8, device="cuda")[off:] for _ in range(m)]
+        ecg.dev_matrix_encode(k, m, M, dev_data, dev_cod, B)
+        torch.cuda.synchronize()
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode(k, m, M, host, ref, B)
+        assert same([c.cpu().numpy() for c in dev_cod], ref), (B, off)
+        # decode on device, in place
+        for pat in ([3], [0, 11], [10, 12, 13, 1]):
+            dd = [d.clone() for d in dev_data] + [c.clone() for c in dev_cod]
+            for i in pat:
+                dd[i].fill_(0)
+            assert ecg.dev_matrix_decode(k, m, M, 1, pat + [-1], dd[:k], dd[k:], B) == 0
+            torch.cuda.synchronize()
+            assert same([x.cpu().numpy() for x in dd], host + ref), pat
+
+
+def test_facade_device_tier(ecg, oracle, torch_cuda):
+    torch = torch_cuda
+    from oracle import ec_ref as E
+    B = 8192
+    for name, t, params in CODES:
+        o, p = _pair(t, params)
+        data = E.blocks(o.k, B, 5)
+        coding = E.zeros(o.m, B)
+        o.encode(data, coding, B)
+        dd = [torch.from_numpy(x).cuda() for x in data]
+        dc = [torch.zeros(B, dtype=torch.uint8, device="cuda") for _ in range(o.m)]
+        assert p.encode(dd, dc, B) == 0
+        torch.cuda.synchronize()
+        assert same([c.cpu().numpy() for c in dc], coding), name
+
+
+def test_fill_random_matches_oracle(ecg, oracle, torch_cuda):
+    torch = torch_cuda
+    for n, off in [(1, 0), (13, 5), (1 << 20, 123456)]:
+        t = torch.empty(n, dtype=torch.uint8, device="cuda")
+        ecg.fill_random(t, 0xEC0DE, off)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), oracle.splitmix_bytes(0xEC0DE, off, n))
+
+
+def test_encode_batch_vs_oracle(ecg, oracle, torch_cuda):
+    torch = torch_cuda
+    k, m, B, S = 10, 4, 1 << 20, 6
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    d_in = torch.empty((S, k, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(d_in, 7)
+    d_out = torch.empty((S, m, B), dtype=torch.uint8, device="cuda")
+    ecg.encode_batch(k, m, M, d_in, d_out)
+    torch.cuda.synchronize()
+    hin, hout = d_in.cpu().numpy(), d_out.cpu().numpy()
+    for s in range(S):
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode_simd(k, m, M, [hin[s, j] for j in range(k)], ref, B)
+        assert same([hout[s, i] for i in range(m)], ref), s
+
+
+def test_decode_batch_rotating_patterns(ecg, oracle, torch_cuda):
+    torch = torch_cuda
+    k, m, B, S = 10, 4, 65536 + 16, 28
+    n = k + m
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(stripes[:, :k], 1)  # non-contiguous view fill is not allowed -> fill whole then encode
+    ecg.fill_random(stripes, 1)
+    ecg.encode_batch(k, m, M, stripes[:, :k], stripes[:, k:])
+    patterns = [[e] for e in range(n)]
+    pos = torch.arange(S, device="cuda", dtype=torch.int32) % n
+    out = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
+    ecg.decode_batch(k, m, M, 1, patterns, stripes, out=out, pattern_of_stripe=pos)
+    torch.cuda.synchronize()
+    for s in range(S):
+        assert torch.equal(out[s, 0], stripes[s, s % n]), s
+    # in place, pairs of erasures, stripes padded (block stride > B)
+    pad = torch.zeros((4, n, B + 48), dtype=torch.uint8, device="cuda")
+    view = pad[:, :, :B]
+    view.copy_(stripes[:4])
+    orig = view.clone()
+    view[:, 2].zero_()
+    view[:, 12].zero_()
+    ecg.decode_batch(k, m, M, 1, [[2, 12]], view)
+    torch.cuda.synchronize()
+    assert torch.equal(view, orig)
+
+
+def test_matrix_apply_and_addition_batch(ecg, oracle, torch_cuda):
+    torch = torch_cuda
+    B, S = 4096, 16
+    d_in = torch.empty((S, 6, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(d_in, 9)
+    coef = [[1, 7, 0, 255], [0, 0, 1, 1]]
+    out = torch.zeros((S, 3, B), dtype=torch.uint8, device="cuda")
+    ecg.matrix_apply_batch(coef, [5, 1, 2, 0], [2, 0], d_in, out)
+    add = torch.zeros((S, 2, B), dtype=torch.uint8, device="cuda")
+    ecg.perform_addition_batch(6, 2, d_in, add)
+    torch.cuda.synchronize()
+    hin, hout, hadd = d_in.cpu().numpy(), out.cpu().numpy(), add.cpu().numpy()
+    for s in range(S):
+        src = [hin[s, i] for i in (5, 1, 2, 0)]
+        ref = [np.zeros(B, np.uint8) for _ in range(2)]
+        oracle.jerasure_matrix_encode(4, 2, [c for r in coef for c in r], src, ref, B)
+        assert np.array_equal(hout[s, 2], ref[0]) and np.array_equal(hout[s, 0], ref[1])
+        assert not hout[s, 1].any()
+        for i in range(2):
+            assert np.array_equal(hadd[s, i], hin[s, i] ^ hin[s, i + 2] ^ hin[s, i + 4])
+
+
+def test_threads_concurrent_host_calls(ecg, oracle, torch_cuda):
+    """The proxy runs EC calls on detached threads (proxy.cpp:416-419): concurrent host-tier calls."""
+    k, m, B = 6, 4, 1 << 16
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    errors = []
+
+    def worker(t):
+        try:
+            for it in range(5):
+                data = [rnd(B, 1000 * t + 10 * it + j) for j in range(k)]
+                a = [np.zeros(B, np.uint8) for _ in range(m)]
+                b = [np.zeros(B, np.uint8) for _ in range(m)]
+                oracle.jerasure_matrix_encode(k, m, M, data, a, B)
+                ecg.jerasure_matrix_encode(k, m, M, data, b, B)
+                if not same(a, b):
+                    errors.append((t, it))
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    assert not errors
+
+
+def test_full_size_rs10_4_round_trip(ecg, oracle, torch_cuda):
+    """BASELINE config 2 at full size: RS(10,4), 1 MiB blocks, 4096 stripes (56 GiB in HBM).
+    encode -> rotate one erasure per stripe (s mod 14) -> decode -> equals the original block; three
+    sampled stripes also checked byte-for-byte against the oracle."""
+    torch = torch_cuda
+    k, m, B, S = 10, 4, 1 << 20, 4096
+    n = k + m
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(stripes, 0xEC0DE)
+    ecg.encode_batch(k, m, M, stripes[:, :k], stripes[:, k:])
+    pos = (torch.arange(S, device="cuda", dtype=torch.int32) % n).contiguous()
+    out = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
+    ecg.decode_batch(k, m, M, 1, [[e] for e in range(n)], stripes, out=out, pattern_of_stripe=pos)
+    torch.cuda.synchronize()
+    idx = torch.arange(S, device="cuda") % n
+    expect = stripes[torch.arange(S, device="cuda"), idx]
+    assert torch.equal(out[:, 0], expect)
+    for s in (0, 1234, S - 1):
+        h = stripes[s].cpu().numpy()
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode_simd(k, m, M, [h[j] for j in range(k)], ref, B)
+        assert same([h[k + i] for i in range(m)], ref), s
+    del stripes, out, expect
+    torch.cuda.empty_cache()
