@@ -124,7 +124,7 @@ __device__ __forceinline__ void fold_general(const uint32_t (&x)[U][4], const EC
 }
 
 // BINARY flavour (every coefficient 0 or 1: perform_addition, LRC local rows, PC merges):
-// acc ^= x & mask in one v_bitop3 (truth table 0x6a = a ^ (b & c)), mask = 0 or ~0 from SGPRs.
+// acc ^= x & mask in one v_bitop3 (LUT index = S0<<2 | S1<<1 | S2, so a ^ (b & c) = 0x78), mask = 0 or ~0 from SGPRs.
 template <int MT, int U>
 __device__ __forceinline__ void fold_binary(const uint32_t (&x)[U][4], const ECG_CONST CoefTab* t,
                                             uint32_t (&acc)[MT][4]) {
@@ -134,7 +134,7 @@ __device__ __forceinline__ void fold_binary(const uint32_t (&x)[U][4], const ECG
         for (int p = 0; p < MT; ++p) {
             const uint32_t msk = t[u * MT + p].mask;
 #pragma unroll
-            for (int d = 0; d < 4; ++d) acc[p][d] = __builtin_amdgcn_bitop3_b32(acc[p][d], x[u][d], msk, 0x6a);
+            for (int d = 0; d < 4; ++d) acc[p][d] = __builtin_amdgcn_bitop3_b32(acc[p][d], x[u][d], msk, 0x78);
         }
 }
 
