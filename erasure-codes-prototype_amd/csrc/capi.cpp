@@ -42,6 +42,9 @@ int ecg_set_device(int device) { return hipSetDevice(device) == hipSuccess ? ECG
 
 void ecg_free(void* p) { free(p); }
 
+int ecg_set_option(int option, long long value) { return set_option(option, value) == 0 ? ECG_OK : ECG_EINVAL; }
+long long ecg_get_option(int option) { return get_option(option); }
+
 // ------------------------------------------------------------------------------ tier 1
 
 int* ecg_reed_sol_vandermonde_coding_matrix(int k, int m, int w) {

@@ -4,7 +4,7 @@
 //
 // Data path (HBM-bound, no MFMA -- byte-field XOR-multiply, not a dense contraction):
 //   * each lane owns one 16-byte column of every block: one global_load_dwordx4 per input block,
-//     64 lanes = 1 KiB contiguous per wave-instruction, 4 inputs in flight per unrolled step;
+//     64 lanes = 1 KiB contiguous per wave-instruction;
 //   * m_out accumulators of 16 bytes stay in VGPRs, so every input byte is read from HBM once and
 //     every output byte written once ((k + m) * B bytes per stripe: the algorithmic minimum);
 //   * the multiply is three v_perm_b32 table lookups per dword (bit fields [2:0], [5:3], [7:6]) with
@@ -13,9 +13,14 @@
 //   * straight-line code (no per-coefficient branches); matrices whose entries are all 0/1
 //     (perform_addition, LRC local rows, PC merges) take a BINARY flavour: one v_bitop3
 //     acc ^ (x & mask) per coefficient-dword.
+//   * grid: one 256-thread workgroup per 4 KiB chunk of every block of a stripe (cols_per_wg = 256),
+//     workgroups mapped XCD-contiguously (grid_map 1), non-temporal loads and stores -- measured
+//     best on MI355X (profiles/r01/microbench.*: 6.1 TB/s encode vs 5.3 TB/s for 16 KiB chunks).
 // VALU cost per 16-byte column: 20 ops to split one input, ~18 per coefficient (GENERAL) or 4
 // (BINARY); for RS(10,4) encode ~1000 ops per 160 data bytes, ~35 % of gfx950's integer issue rate
 // at the HBM roofline.
+#include <atomic>
+
 #include "gf_kernels.hpp"
 #include "gf256.hpp"
 
@@ -58,26 +63,27 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-// gfx950 v_bitop3_b32 with truth table 0x96 = a ^ b ^ c in one VALU op.
+// gfx950 v_bitop3_b32, LUT index = S0<<2 | S1<<1 | S2.  0x96 = a ^ b ^ c.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool NT>
+// NT policy bits: 1 = non-temporal loads, 2 = non-temporal stores.
+template <int NT>
 __device__ __forceinline__ void load16(const uint8_t* p, uint32_t (&x)[4]) {
     u32x4 v;
-    if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    if constexpr (NT & 1) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     else v = *reinterpret_cast<const u32x4*>(p);
     x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
 }
 
-template <bool NT>
+template <int NT>
 __device__ __forceinline__ void store16(uint8_t* p, const uint32_t (&x)[4]) {
     u32x4 v;
     v.x = x[0]; v.y = x[1]; v.z = x[2]; v.w = x[3];
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    if constexpr (NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
     else *reinterpret_cast<u32x4*>(p) = v;
 }
 
@@ -95,36 +101,34 @@ __device__ __forceinline__ uint32_t gmul(const ECG_CONST CoefTab& t, const Split
     return xor3(perm(t.t0hi, t.t0lo, s.i0), perm(t.t1hi, t.t1lo, s.i1), perm(t.t2, t.t2, s.i2));
 }
 
-// GENERAL flavour: U inputs (U = 1, 2 or 4) folded into MT accumulators.  Straight-line: every
-// coefficient goes through the tables (c = 0 and c = 1 tables are exact), products of input pairs
-// are folded with one v_bitop3 each so a coefficient costs 3 perm + 1.5 bitop3 per dword.
+// GENERAL flavour: U inputs folded into MT accumulators, input pairs share one v_bitop3.  Every
+// coefficient goes through the tables (c = 0 and c = 1 tables are exact).
 template <int MT, int U>
 __device__ __forceinline__ void fold_general(const uint32_t (&x)[U][4], const ECG_CONST CoefTab* t,
                                              uint32_t (&acc)[MT][4]) {
-    if constexpr (U == 1) {
+#pragma unroll
+    for (int u = 0; u + 1 < U; u += 2) {
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-            const Split s0 = split(x[0][d]);
+            const Split s0 = split(x[u][d]);
+            const Split s1 = split(x[u + 1][d]);
 #pragma unroll
-            for (int p = 0; p < MT; ++p) acc[p][d] ^= gmul(t[p], s0);
+            for (int p = 0; p < MT; ++p)
+                acc[p][d] = xor3(acc[p][d], gmul(t[u * MT + p], s0), gmul(t[(u + 1) * MT + p], s1));
         }
-    } else {
+    }
+    if constexpr (U & 1) {
 #pragma unroll
-        for (int u = 0; u < U; u += 2) {
+        for (int d = 0; d < 4; ++d) {
+            const Split s0 = split(x[U - 1][d]);
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const Split s0 = split(x[u][d]);
-                const Split s1 = split(x[u + 1][d]);
-#pragma unroll
-                for (int p = 0; p < MT; ++p)
-                    acc[p][d] = xor3(acc[p][d], gmul(t[u * MT + p], s0), gmul(t[(u + 1) * MT + p], s1));
-            }
+            for (int p = 0; p < MT; ++p) acc[p][d] ^= gmul(t[(U - 1) * MT + p], s0);
         }
     }
 }
 
 // BINARY flavour (every coefficient 0 or 1: perform_addition, LRC local rows, PC merges):
-// acc ^= x & mask in one v_bitop3 (LUT index = S0<<2 | S1<<1 | S2, so a ^ (b & c) = 0x78), mask = 0 or ~0 from SGPRs.
+// acc ^= x & mask in one v_bitop3 (0x78 = S0 ^ (S1 & S2)), mask = 0 or ~0 from SGPRs.
 template <int MT, int U>
 __device__ __forceinline__ void fold_binary(const uint32_t (&x)[U][4], const ECG_CONST CoefTab* t,
                                             uint32_t (&acc)[MT][4]) {
@@ -144,12 +148,36 @@ __device__ __forceinline__ void fold(const uint32_t (&x)[U][4], const ECG_CONST 
     else fold_general<MT, U>(x, t, acc);
 }
 
-// Vector path: bytes [0, 16 * floor(B / 16)) of every block; all pointers 16-byte aligned.
+constexpr int occupancy_for(int MT) { return MT <= 4 ? 6 : 4; }
+
+// Workgroup -> (stripe, column chunk).  grid_map 0: linear (workgroup b takes chunk b).  grid_map 1:
+// XCD-contiguous -- the dispatcher deals workgroups round-robin over the 8 XCDs, so b % 8 names the
+// XCD group; each group is given a contiguous 1/8 of the chunk list (T1 in the HIP guide; here for
+// DRAM locality of the concurrently active chunks, not L2 reuse).  Speed only, never correctness.
+__device__ __forceinline__ void wg_coords(const GfLaunch& a, int& s, int& w) {
+    long long b = blockIdx.x;
+    if (a.grid_map == 1) {
+        const long long G = (long long)gridDim.x;
+        const long long per = G >> 3;  // G % 8 == 0 is checked by the host
+        b = (b & 7) * per + (b >> 3);
+    } else if (a.grid_map == 2) {  // stripe s runs on XCD group s % 8 (S % 8 == 0 checked by the host)
+        const long long i = b >> 3;
+        const long long srow = i / a.wg_per_stripe;
+        s = (int)(srow * 8 + (b & 7));
+        w = (int)(i - srow * a.wg_per_stripe);
+        return;
+    }
+    s = (int)(b / a.wg_per_stripe);
+    w = (int)(b - (long long)s * a.wg_per_stripe);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic vector path: bytes [0, 16 * floor(B / 16)) of every block; all pointers 16-byte aligned.
 // grid.x = S * wg_per_stripe (stripe-major), grid.y = row tiles of MT outputs.
-template <int MT, int MODE, bool NT, bool BIN>
-__global__ void __launch_bounds__(kThreads, (MT <= 4 ? 6 : 4)) gf_vec_kernel(const GfLaunch a) {
-    const int s = blockIdx.x / a.wg_per_stripe;
-    const int w = blockIdx.x - s * a.wg_per_stripe;
+template <int MT, int MODE, int NT, bool BIN>
+__global__ void __launch_bounds__(kThreads, occupancy_for(MT)) gf_vec_kernel(const GfLaunch a) {
+    int s, w;
+    wg_coords(a, s, w);
     const int rt = blockIdx.y;
     const int prog = a.prog_of_stripe ? cst(a.prog_of_stripe)[s] : 0;
     const int k = a.k;
@@ -200,8 +228,8 @@ __global__ void __launch_bounds__(kThreads, (MT <= 4 ? 6 : 4)) gf_vec_kernel(con
 // Byte path: bytes [off0, B) (tails, unaligned pointers).  cols_per_wg = bytes per workgroup.
 template <int MT, int MODE, bool BIN>
 __global__ void __launch_bounds__(kThreads) gf_byte_kernel(const GfLaunch a) {
-    const int s = blockIdx.x / a.wg_per_stripe;
-    const int w = blockIdx.x - s * a.wg_per_stripe;
+    int s, w;
+    wg_coords(a, s, w);
     const int rt = blockIdx.y;
     const int prog = a.prog_of_stripe ? cst(a.prog_of_stripe)[s] : 0;
     const int k = a.k;
@@ -250,60 +278,103 @@ __global__ void __launch_bounds__(kThreads) fill_splitmix_kernel(uint8_t* dst, l
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Dispatch
+
+std::atomic<long long> g_opt[ECG_OPT_COUNT] = {};
+std::atomic<int> g_opt_init{0};
+
+void init_options() {
+    if (g_opt_init.load(std::memory_order_acquire)) return;
+    auto env = [](const char* n, long long d) {
+        const char* e = getenv(n);
+        return e ? atoll(e) : d;
+    };
+    g_opt[ECG_OPT_NT].store(env("ECG_NT", 3));
+    g_opt[ECG_OPT_COLS_PER_WG].store(env("ECG_COLS_PER_WG", 0));
+    g_opt[ECG_OPT_GRID_MAP].store(env("ECG_GRID_MAP", 1));
+    g_opt_init.store(1, std::memory_order_release);
+}
+
+using Launcher = void (*)(const GfLaunch&, dim3, hipStream_t);
+
+template <typename F>
+void launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL(kernel, grid, dim3(kThreads), 0, st, a);
+}
+
+template <int MT, int MODE, int NT, bool BIN>
+void gen_launch(const GfLaunch& a, dim3 g, hipStream_t st) { launch_with(gf_vec_kernel<MT, MODE, NT, BIN>, a, g, st); }
+
+template <int MODE, int NT, bool BIN>
+Launcher gen_pick(int MT) {
+    switch (MT) {
+        case 1: return gen_launch<1, MODE, NT, BIN>;
+        case 2: return gen_launch<2, MODE, NT, BIN>;
+        case 3: return gen_launch<3, MODE, NT, BIN>;
+        case 4: return gen_launch<4, MODE, NT, BIN>;
+        case 5: return gen_launch<5, MODE, NT, BIN>;
+        case 6: return gen_launch<6, MODE, NT, BIN>;
+        case 7: return gen_launch<7, MODE, NT, BIN>;
+        case 8: return gen_launch<8, MODE, NT, BIN>;
+        default: return nullptr;
+    }
+}
+
+template <int MODE, int NT>
+Launcher pick_vec_nt(const GfLaunch& a) {
+    return a.binary ? gen_pick<MODE, NT, true>(a.MT) : gen_pick<MODE, NT, false>(a.MT);
+}
+
+template <int MODE>
+Launcher pick_vec(const GfLaunch& a, int nt) {
+    switch (nt & 3) {
+        case 0: return pick_vec_nt<MODE, 0>(a);
+        case 1: return pick_vec_nt<MODE, 1>(a);
+        case 2: return pick_vec_nt<MODE, 2>(a);
+        default: return pick_vec_nt<MODE, 3>(a);
+    }
+}
+
 template <int MT, int MODE, bool BIN>
-hipError_t dispatch_vec(const GfLaunch& a, dim3 grid, bool nt, hipStream_t st) {
-    if (nt) hipLaunchKernelGGL((gf_vec_kernel<MT, MODE, true, BIN>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((gf_vec_kernel<MT, MODE, false, BIN>), grid, dim3(kThreads), 0, st, a);
-    return hipGetLastError();
-}
+void byte_launch(const GfLaunch& a, dim3 g, hipStream_t st) { launch_with(gf_byte_kernel<MT, MODE, BIN>, a, g, st); }
 
 template <int MODE, bool BIN>
-hipError_t dispatch_vec_mt(const GfLaunch& a, dim3 grid, bool nt, hipStream_t st) {
-    switch (a.MT) {
-        case 1: return dispatch_vec<1, MODE, BIN>(a, grid, nt, st);
-        case 2: return dispatch_vec<2, MODE, BIN>(a, grid, nt, st);
-        case 3: return dispatch_vec<3, MODE, BIN>(a, grid, nt, st);
-        case 4: return dispatch_vec<4, MODE, BIN>(a, grid, nt, st);
-        case 5: return dispatch_vec<5, MODE, BIN>(a, grid, nt, st);
-        case 6: return dispatch_vec<6, MODE, BIN>(a, grid, nt, st);
-        case 7: return dispatch_vec<7, MODE, BIN>(a, grid, nt, st);
-        case 8: return dispatch_vec<8, MODE, BIN>(a, grid, nt, st);
-        default: return hipErrorInvalidValue;
+Launcher pick_byte_bin(int MT) {
+    switch (MT) {
+        case 1: return byte_launch<1, MODE, BIN>;
+        case 2: return byte_launch<2, MODE, BIN>;
+        case 3: return byte_launch<3, MODE, BIN>;
+        case 4: return byte_launch<4, MODE, BIN>;
+        case 5: return byte_launch<5, MODE, BIN>;
+        case 6: return byte_launch<6, MODE, BIN>;
+        case 7: return byte_launch<7, MODE, BIN>;
+        case 8: return byte_launch<8, MODE, BIN>;
+        default: return nullptr;
     }
 }
 
 template <int MODE>
-hipError_t dispatch_vec_bin(const GfLaunch& a, dim3 grid, bool nt, hipStream_t st) {
-    return a.binary ? dispatch_vec_mt<MODE, true>(a, grid, nt, st) : dispatch_vec_mt<MODE, false>(a, grid, nt, st);
-}
-
-template <int MODE, bool BIN>
-hipError_t dispatch_byte_mt(const GfLaunch& a, dim3 grid, hipStream_t st) {
-#define ECG_BYTE_CASE(N) \
-    case N: hipLaunchKernelGGL((gf_byte_kernel<N, MODE, BIN>), grid, dim3(kThreads), 0, st, a); break;
-    switch (a.MT) {
-        ECG_BYTE_CASE(1) ECG_BYTE_CASE(2) ECG_BYTE_CASE(3) ECG_BYTE_CASE(4)
-        ECG_BYTE_CASE(5) ECG_BYTE_CASE(6) ECG_BYTE_CASE(7) ECG_BYTE_CASE(8)
-        default: return hipErrorInvalidValue;
-    }
-#undef ECG_BYTE_CASE
-    return hipGetLastError();
-}
-
-template <int MODE>
-hipError_t dispatch_byte_bin(const GfLaunch& a, dim3 grid, hipStream_t st) {
-    return a.binary ? dispatch_byte_mt<MODE, true>(a, grid, st) : dispatch_byte_mt<MODE, false>(a, grid, st);
-}
-
-bool use_nt_default() {
-    static const int v = [] {
-        const char* e = getenv("ECG_NT");
-        return e ? atoi(e) : 1;
-    }();
-    return v != 0;
+Launcher pick_byte(const GfLaunch& a) {
+    return a.binary ? pick_byte_bin<MODE, true>(a.MT) : pick_byte_bin<MODE, false>(a.MT);
 }
 
 }  // namespace
+
+long long get_option(int opt) {
+    init_options();
+    if (opt < 0 || opt >= ECG_OPT_COUNT) return -1;
+    return g_opt[opt].load();
+}
+
+int set_option(int opt, long long value) {
+    init_options();
+    if (opt < 0 || opt >= ECG_OPT_COUNT) return -1;
+    if (opt == ECG_OPT_NT && (value < 0 || value > 3)) return -1;
+    if (opt == ECG_OPT_COLS_PER_WG && (value < 0 || (value % kThreads) != 0)) return -1;
+    g_opt[opt].store(value);
+    return 0;
+}
 
 hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st) {
     if (base.k < 1 || base.m < 1 || base.S < 1 || base.B < 0 || base.MT < 1 || base.MT > kMaxMT)
@@ -311,26 +382,32 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
     if (mode == GF_MODE_INLINE && (base.S != 1 || base.k > kInlineSrc || base.m > kInlineDst))
         return hipErrorInvalidValue;
     if (base.B == 0) return hipSuccess;
+    init_options();
     GfLaunch a = base;
     const long long vec_bytes = vec_ok ? (a.B & ~15LL) : 0;
     if (vec_bytes > 0) {
         const long long ncols = vec_bytes >> 4;
-        long long cpw = 4LL * kThreads;                       // 16 KiB of every block per workgroup
+        long long cpw = g_opt[ECG_OPT_COLS_PER_WG].load();
+        if (cpw <= 0) cpw = kThreads;  // 4 KiB of every block per workgroup (measured best, r01 microbench)
         if (ncols < cpw) cpw = ((ncols + kThreads - 1) / kThreads) * kThreads;
         a.cols_per_wg = (int)cpw;
         a.wg_per_stripe = (int)((ncols + cpw - 1) / cpw);
         a.off0 = 0;
         const long long gx = (long long)a.S * a.wg_per_stripe;
         if (gx > 0x7fffffffLL) return hipErrorInvalidConfiguration;
-        dim3 grid((unsigned)gx, (unsigned)a.rtiles);
-        const bool nt = use_nt_default();
-        hipError_t e;
+        const long long gm = g_opt[ECG_OPT_GRID_MAP].load();
+        a.grid_map = (gm == 1 && gx % 8 == 0) ? 1 : (gm == 2 && a.S % 8 == 0) ? 2 : 0;
+        const int nt = (int)g_opt[ECG_OPT_NT].load();
+        Launcher l = nullptr;
         switch (mode) {
-            case GF_MODE_INLINE: e = dispatch_vec_bin<GF_MODE_INLINE>(a, grid, nt, st); break;
-            case GF_MODE_PTRS: e = dispatch_vec_bin<GF_MODE_PTRS>(a, grid, nt, st); break;
-            case GF_MODE_STRIDED: e = dispatch_vec_bin<GF_MODE_STRIDED>(a, grid, nt, st); break;
+            case GF_MODE_INLINE: l = pick_vec<GF_MODE_INLINE>(a, nt); break;
+            case GF_MODE_PTRS: l = pick_vec<GF_MODE_PTRS>(a, nt); break;
+            case GF_MODE_STRIDED: l = pick_vec<GF_MODE_STRIDED>(a, nt); break;
             default: return hipErrorInvalidValue;
         }
+        if (!l) return hipErrorInvalidValue;
+        l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     if (vec_bytes < a.B) {
@@ -340,16 +417,19 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         a.cols_per_wg = (int)bpw;
         a.wg_per_stripe = (int)((nbytes + bpw - 1) / bpw);
         a.off0 = vec_bytes;
+        a.grid_map = 0;
         const long long gx = (long long)a.S * a.wg_per_stripe;
         if (gx > 0x7fffffffLL) return hipErrorInvalidConfiguration;
-        dim3 grid((unsigned)gx, (unsigned)a.rtiles);
-        hipError_t e;
+        Launcher l = nullptr;
         switch (mode) {
-            case GF_MODE_INLINE: e = dispatch_byte_bin<GF_MODE_INLINE>(a, grid, st); break;
-            case GF_MODE_PTRS: e = dispatch_byte_bin<GF_MODE_PTRS>(a, grid, st); break;
-            case GF_MODE_STRIDED: e = dispatch_byte_bin<GF_MODE_STRIDED>(a, grid, st); break;
+            case GF_MODE_INLINE: l = pick_byte<GF_MODE_INLINE>(a); break;
+            case GF_MODE_PTRS: l = pick_byte<GF_MODE_PTRS>(a); break;
+            case GF_MODE_STRIDED: l = pick_byte<GF_MODE_STRIDED>(a); break;
             default: return hipErrorInvalidValue;
         }
+        if (!l) return hipErrorInvalidValue;
+        l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/ecg.h"
+
 namespace ecg {
 
 // Per-coefficient multiply tables for v_perm_b32 (one 32-byte record, loaded into SGPRs).
@@ -55,9 +57,14 @@ struct GfLaunch {
     int k, m, S;
     int MT, rtiles;
     int binary;          // every coefficient is 0 or 1 -> BINARY kernel flavour
+    int grid_map;        // 0 linear, 1 XCD-contiguous workgroup -> chunk mapping
     int wg_per_stripe;
     int cols_per_wg;     // 16-byte columns per workgroup (vector path) / bytes per workgroup (byte path)
 };
+
+// Runtime tuning options (ecg_set_option): see ECG_OPT_* in include/ecg.h.
+long long get_option(int opt);
+int set_option(int opt, long long value);
 
 // Launch the region product over bytes [0, B) of every stripe.  `vec_ok` = every block pointer is
 // 16-byte aligned (the host checks); otherwise the byte path covers everything.  Returns a hipError_t.

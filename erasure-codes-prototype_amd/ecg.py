@@ -32,12 +32,16 @@ ECG_EUNDECODABLE = -1
 ECG_EINVAL = -2
 ECG_EHIP = -3
 ECG_EUNPINNED = -4
+ECG_OPT_NT = 0
+ECG_OPT_COLS_PER_WG = 1
+ECG_OPT_GRID_MAP = 2
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 
 # Every symbol include/ecg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free",
+    "ecg_set_option", "ecg_get_option",
     "ecg_reed_sol_vandermonde_coding_matrix", "ecg_cauchy_good_general_coding_matrix",
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
     "ecg_jerasure_invert_matrix", "ecg_jerasure_matrix_multiply", "ecg_galois_region_xor",
@@ -118,6 +122,8 @@ def lib():
         "ecg_device_count": ([], I),
         "ecg_set_device": ([I], I),
         "ecg_free": ([P], None),
+        "ecg_set_option": ([I, LL], I),
+        "ecg_get_option": ([I], LL),
         "ecg_reed_sol_vandermonde_coding_matrix": ([I, I, I], IP),
         "ecg_cauchy_good_general_coding_matrix": ([I, I, I], IP),
         "ecg_cauchy_original_coding_matrix": ([I, I, I], IP),
@@ -159,6 +165,15 @@ def lib():
         f.restype = res
     _L = L
     return L
+
+
+def set_option(option, value):
+    """Kernel tuning knob (include/ecg.h ECG_OPT_*); never changes results."""
+    return _check(lib().ecg_set_option(option, value), "set_option")
+
+
+def get_option(option):
+    return lib().ecg_get_option(option)
 
 
 def _ints(vals):

@@ -42,6 +42,15 @@ int ecg_device_count(void);
 int ecg_set_device(int device);    /* selects the HIP device for the calling thread */
 void ecg_free(void* p);            /* frees matrices returned by this library (malloc'd, like Jerasure) */
 
+/* Kernel tuning options (process-wide; defaults also settable through the environment variables
+ * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP).  Results never depend on them. */
+#define ECG_OPT_NT 0           /* non-temporal policy: bit 0 = loads, bit 1 = stores (default 3) */
+#define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 256; 0 = auto (256) */
+#define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous (default), 2 = stripe s on XCD group s%8 */
+#define ECG_OPT_COUNT 3
+int ecg_set_option(int option, long long value);
+long long ecg_get_option(int option);
+
 /* ---------------------------------------------------------------- tier 1: Jerasure-compatible (w = 8)
  * Replaces reed_sol_vandermonde_coding_matrix  (called rs.cpp:7,34,297; lrc.cpp:624,935,1170) */
 int* ecg_reed_sol_vandermonde_coding_matrix(int k, int m, int w);

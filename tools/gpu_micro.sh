@@ -1,0 +1,11 @@
+#!/bin/bash
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600 > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/pytest_gpu.log | tail -20
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 600 python tools/microbench.py --out gpurun_out/micro.json > gpurun_out/micro.log 2>&1
+rc=$?; echo "micro rc=$rc"; cat gpurun_out/micro.log | grep -v amdgpu.ids
+exit $rc
