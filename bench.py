@@ -1,24 +1,27 @@
 #!/usr/bin/env python3
-"""bench.py — BASELINE.json's headline metric on MI355X.
+"""bench.py — BASELINE.json's headline metric on MI355X (plus the other BASELINE configs on request).
 
-Metric: "GiB/s encode + single-block decode (device-resident), RS(10,4) 1 MiB blocks, 1 & 8 GPU".
-Workload (BASELINE.json configs[1]): RS(k=10, m=4), block_size = 1 MiB, a batch of S = 4096 stripes
-per GPU resident in HBM ([S][14][1 MiB] = 56 GiB + a 4 GiB rebuild buffer).  One step = one pass of
-the hot path over the batch:
-  1. encode:  jerasure_matrix_encode of every stripe   (ecg_encode_batch, one launch)
-  2. decode:  every stripe loses block e = s mod 14 and rebuilds it with jerasure_matrix_decode
-              semantics (row_k_ones = failed_num, rs.cpp:36) into the rebuild buffer
-              (ecg_decode_batch, 14 composed patterns, one launch)
-value = data bytes coded per second over all ranks = N * S * 2 * k * B / t_max  (GiB/s; each pass
-reads k data-sized blocks per stripe).  Inputs are synthetic splitmix64 bytes generated on the GPU
-before the timed region.
+Default workload (BASELINE.json configs[1], what the driver runs):
+  RS(k=10, m=4), block_size = 1 MiB, S = 4096 stripes per GPU resident in HBM ([S][14][1 MiB] = 56 GiB
+  + a 4 GiB rebuild buffer).  One step = one pass of the hot path over the batch:
+    1. encode: jerasure_matrix_encode of every stripe                         (ecg_encode_batch)
+    2. decode: stripe s loses block e = s mod 14 and rebuilds it with jerasure_matrix_decode semantics
+       (row_k_ones = failed_num, rs.cpp:36) into the rebuild buffer  (ecg_decode_batch, 14 patterns)
+  value = N * S * 2 * k * B / t_max in GiB/s (each pass reads k data-sized blocks per stripe).
+  Inputs: splitmix64 bytes generated on the GPU before the timed region.
 
-Multi-GPU: stripes are independent, so each rank runs its own S stripes (weak scaling, no data-path
-collective); one barrier + synchronize brackets the timed region, the elapsed time is max-reduced.
+Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line):
+  lrc-repair  configs[2]: Azure-LRC(12,2,2), 1 MiB, single-block repair of block s mod 16 of every
+              stripe, partial_decoding=true (helper partials + main partial + perform_addition) and the
+              fused single-launch form;
+  pc-merge    configs[3]: PC(4,1,4,1), 4 MiB blocks, stripe merging x=2 (HORIZONTAL): the 5 row
+              parities of the merged PC(8,1,4,1) recomputed from the two old stripes;
+  rs4m-waves  configs[4]: RS(10,4), 4 MiB blocks, 65536 stripes split over the ranks, encoded in
+              HBM-resident waves of 1024 stripes (input regenerated per wave outside the timing).
 
-Extra JSON fields: roofline (dominant kernel = the encode kernel, timed with HIP events on the
-stream it runs on; algorithmic bytes = (k+m)*B per stripe), cpu_baseline (oracle CPU restatement of
-the same step on a bounded sample, rank 0 at N=1 only).
+Multi-GPU: one process per GPU (torch.distributed.run), stripes sharded per rank (ecg_dist), no
+data-path collective: barrier + synchronize around the timed region, elapsed time max-reduced,
+per-rank parity checksums all-gathered.
 """
 import argparse
 import json
@@ -31,12 +34,13 @@ sys.path.insert(0, os.path.join(ROOT, "erasure-codes-prototype_amd"))
 sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 import ecg  # noqa: E402
+import ecg_dist as D  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+METRIC = "GiB/s encode + single-block decode (device-resident), RS(10,4) 1 MiB blocks, 1 & 8 GPU"
 
 
 def parse():
@@ -44,19 +48,50 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU (BASELINE configs[1]: 4096)")
-    ap.add_argument("--block-size", type=int, default=1 << 20)
-    ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--workload", default="rs-encode-decode",
+                    choices=["rs-encode-decode", "lrc-repair", "pc-merge", "rs4m-waves"])
+    ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
+    ap.add_argument("--block-size", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
 
 
+def events(n):
+    return [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(n)]
+
+
+def timed_loop(r, steps, step):
+    """barrier + synchronize, K steps (each records its own events), synchronize + barrier; max over ranks."""
+    evs = events(steps)
+    D.barrier(r)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    D.barrier(r)
+    elapsed = time.perf_counter() - t0
+    return D.max_over_ranks(elapsed, r, device="cuda"), evs
+
+
+def pmc_traffic(tag, workload_key):
+    if os.path.exists(PMC_FILE):
+        try:
+            pm = json.load(open(PMC_FILE))
+            if pm.get("workload") == workload_key:
+                return pm.get(f"{tag}_hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+# ------------------------------------------------------------------------------- CPU baseline
+
 def cpu_baseline(k, m, B, target_s):
-    """Oracle CPU restatement (Jerasure algorithm, SIMD split tables) of the same step on a bounded
-    sample: encode + single-erasure decode of S_cpu stripes, one jerasure call per stripe, threads =
-    min(16, cpu_count)."""
+    """Oracle CPU restatement (Jerasure algorithm, gf-complete-style SPLIT(8,4) PSHUFB region multiply)
+    of the same step on a bounded sample: encode + single-erasure decode of S_cpu stripes, one
+    jerasure call per stripe, threads = min(16, cpu_count)."""
     import numpy as np
     from oracle import ref
     ref.build()
@@ -86,30 +121,21 @@ def cpu_baseline(k, m, B, target_s):
                       f"one jerasure call per stripe, {threads} host threads, {t_total:.1f} s"}
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    ecg.lib().ecg_set_device(torch.cuda.current_device())
-    k, m, B, S = a.k, a.m, a.block_size, a.stripes
+# ------------------------------------------------------------------------------- config 2 (default)
+
+def rs_encode_decode(a, r):
+    k, m = 10, 4
+    B = a.block_size or (1 << 20)
+    S = a.stripes or 4096
     n = k + m
     M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
-
     stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
     rebuilt = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
-    ecg.fill_random(stripes, 0xEC0DE, word_offset=rank * (S * n * B // 8))
+    first = r.rank * S  # weak scaling: rank r holds global stripes [r*S, (r+1)*S)
+    ecg.fill_random(stripes, 0xEC0DE, word_offset=D.data_word_offset(first, n, B))
     pattern_of_stripe = (torch.arange(S, device="cuda", dtype=torch.int32) % n).contiguous()
     patterns = [[e] for e in range(n)]
     data, coding = stripes[:, :k], stripes[:, k:]
-
-    # HIP events on torch's current stream, which is the stream ecg launches on (ecg._stream)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
 
     def step(ev=None):
         if ev:
@@ -124,75 +150,259 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    # sanity: the rebuilt blocks equal the erased originals (checked once, outside the timed region)
     idx = torch.arange(S, device="cuda")
-    assert torch.equal(rebuilt[:, 0], stripes[idx, idx % n]), "decode mismatch"
+    assert torch.equal(rebuilt[:, 0], stripes[idx, idx % n]), "decode mismatch"  # outside the timing
+    checks = D.gather_checksums(D.checksum64(coding.contiguous()), r, device="cuda")
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed, evs = timed_loop(r, a.steps, step)
     enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
     dec_ms = [e[1].elapsed_time(e[2]) for e in evs]
-    step_bytes = S * 2 * k * B  # data read by encode + data read by decode
-    value = world * step_bytes * a.steps / elapsed / 2 ** 30
     enc_avg = sum(enc_ms) / len(enc_ms) / 1e3
     dec_avg = sum(dec_ms) / len(dec_ms) / 1e3
-    enc_bytes = S * (k + m) * B          # algorithmic HBM bytes of one encode launch
-    dec_bytes = S * (k + 1) * B          # one decode launch
+    enc_bytes = S * (k + m) * B
+    dec_bytes = S * (k + 1) * B
     achieved = enc_bytes / enc_avg / 1e9
-    traffic = None
-    if os.path.exists(PMC_FILE):
-        try:
-            pm = json.load(open(PMC_FILE))
-            if pm.get("workload") == f"rs{k}{m}_B{B}_S{S}":
-                traffic = pm.get("encode_hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    value = r.world * S * 2 * k * B * a.steps / elapsed / 2 ** 30
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": r.world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 bytes generated on device)",
+        "config": {"workload": f"RS({k},{m}) encode + rotating 1-erasure decode (e = s mod {n})",
+                   "block_size": B, "stripes_per_gpu": S, "global_stripes": S * r.world,
+                   "parallelism": f"stripes sharded over {r.world} GPU(s), no data-path collective"},
+        "encode_gibps_per_gpu": round(S * k * B / enc_avg / 2 ** 30, 2),
+        "decode_gibps_per_gpu": round(S * k * B / dec_avg / 2 ** 30, 2),
+        "encode_ms": round(enc_avg * 1e3, 3), "decode_ms": round(dec_avg * 1e3, 3),
+        "roofline": {"bound": "hbm", "kernel": "gf_vec_kernel<MT=4,STRIDED> (encode)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic("encode", f"rs{k}{m}_B{B}_S{S}"),
+                     "algorithmic_bytes_per_launch": enc_bytes,
+                     "decode_achieved": round(dec_bytes / dec_avg / 1e9, 1),
+                     "decode_frac": round(dec_bytes / dec_avg / 1e9 / HBM_PEAK_GBS, 4),
+                     "decode_traffic": pmc_traffic("decode", f"rs{k}{m}_B{B}_S{S}")},
+        "parity_checksums": [f"{c:016x}" for c in checks],
+    }
+    if r.world == 1 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
+    return line
 
-    if rank == 0:
-        line = {
-            "metric": "GiB/s encode + single-block decode (device-resident), RS(10,4) 1 MiB blocks, 1 & 8 GPU",
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (splitmix64 bytes generated on device)",
-            "config": {"workload": f"RS({k},{m}) encode + rotating 1-erasure decode (e = s mod {n})",
-                       "block_size": B, "stripes_per_gpu": S, "global_stripes": S * world,
-                       "parallelism": f"stripes sharded over {world} GPU(s), no data-path collective"},
-            "encode_gibps_per_gpu": round(S * k * B / enc_avg / 2 ** 30, 2),
-            "decode_gibps_per_gpu": round(S * k * B / dec_avg / 2 ** 30, 2),
-            "encode_ms": round(enc_avg * 1e3, 3),
-            "decode_ms": round(dec_avg * 1e3, 3),
-            "roofline": {"bound": "hbm", "kernel": "gf_vec_kernel<MT=4,STRIDED> (encode)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": enc_bytes,
-                         "decode_achieved": round(dec_bytes / dec_avg / 1e9, 1)},
-        }
-        if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
+
+# ------------------------------------------------------------------------------- config 3
+
+def lrc_repair(a, r):
+    """Azure-LRC(12,2,2), 1 MiB: every stripe loses block e = s mod 16 and repairs it.
+    Data / local-parity loss: local group of 6 survivors.  partial_decoding=true mirrors
+    help_repair/main_repair (handle_repair.cpp:249,375,566): helper partial over the survivors in the
+    helper partition, main partial over the rest, perform_addition of the two.  The fused form computes
+    the repaired block in one launch from the same survivors.  Global-parity loss (12, 13): the global
+    path, re-encode from the 12 data blocks (jerasure_matrix_decode re-encodes erased coding rows)."""
+    k, l, g = 12, 2, 2
+    B = a.block_size or (1 << 20)
+    S = a.stripes or 4096
+    n = k + g + l
+    cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
+    ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)
+    M = ec.make_encoding_matrix()  # (g + l) x k
+    stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(stripes, 0xEC0DE, word_offset=D.data_word_offset(r.rank * S, n, B))
+    ecg.encode_batch(k, g + l, M, stripes[:, :k], stripes[:, k:])
+    rebuilt = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
+    partials = torch.empty((S, 2, B), dtype=torch.uint8, device="cuda")
+    e_of = torch.arange(S, device="cuda", dtype=torch.int32) % n
+    # OPTIMAL partition of Azure(12,2,2) (SURVEY.md §8(d)): {0,1,2},{3,4,5},{6,7,8},{9,10,11},{14,15,12,13}.
+    # A partition other than the failed block's sends one partial when it holds more than f = 1
+    # survivors, otherwise its blocks go to the main proxy directly (handle_repair.cpp:169-176); the
+    # main proxy adds its own partial over its partition's survivors + the direct blocks and XOR-sums
+    # (perform_addition, handle_repair.cpp:371-376).  For every local pattern of this code that gives
+    # exactly two partials of three survivors each.
+    parts = [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9, 10, 11], [14, 15, 12, 13]]
+    fused_progs, part_progs, cls_local = [], ([], []), []
+    for e in range(n):
+        if e in (12, 13):
+            continue
+        gid = e // 6 if e < k else e - 14
+        group = list(range(6 * gid, 6 * gid + 6)) + [14 + gid]
+        surv = [b for b in group if b != e]
+        fused_progs.append((ec.partial_decoding_matrix(surv, surv, [e]), surv, [0]))
+        main_part = next(p for p in parts if e in p)
+        mine = [b for b in surv if b in main_part]
+        helpers = []
+        for p in parts:
+            if p is main_part:
+                continue
+            inside = [b for b in surv if b in p]
+            if len(inside) > 1:
+                helpers.append(inside)
+            else:
+                mine += inside
+        sets = helpers + ([mine] if mine else [])
+        assert len(sets) == 2 and all(len(x) == 3 for x in sets), (e, sets)
+        for i in range(2):
+            part_progs[i].append((ec.partial_decoding_matrix(sets[i], surv, [e]), sets[i], [i]))
+        cls_local.append(e)
+    # class L launch (6 survivors) over stripes with e not in {12, 13}
+    sl = torch.nonzero((e_of != 12) & (e_of != 13)).flatten().to(torch.int32).contiguous()
+    lut = torch.full((n,), -1, dtype=torch.int32)
+    for i, e in enumerate(cls_local):
+        lut[e] = i
+    pl = lut.cuda()[e_of[sl].long()].contiguous()
+    # class G launch (12 data) over stripes with e in {12, 13}
+    sg = torch.nonzero((e_of == 12) | (e_of == 13)).flatten().to(torch.int32).contiguous()
+    pg = (e_of[sg.long()] - 12).contiguous()
+    glob_progs = [(M[i * k:(i + 1) * k], list(range(k)), [0]) for i in range(g)]
+
+    def step_partial(ev=None):
+        if ev:
+            ev[0].record()
+        for i in range(2):  # the two partials (helper proxies / main proxy)
+            ecg.matrix_apply_batch_multi(part_progs[i], stripes, partials, prog_of_stripe=pl, stripe_of=sl)
+        ecg.matrix_apply_batch_multi([([[1, 1]], [0, 1], [0])], partials, rebuilt, stripe_of=sl)  # addition
+        ecg.matrix_apply_batch_multi(glob_progs, stripes, rebuilt, prog_of_stripe=pg, stripe_of=sg)
+        if ev:
+            ev[1].record()
+
+    def step_fused(ev=None):
+        if ev:
+            ev[0].record()
+        ecg.matrix_apply_batch_multi(fused_progs, stripes, rebuilt, prog_of_stripe=pl, stripe_of=sl)
+        ecg.matrix_apply_batch_multi(glob_progs, stripes, rebuilt, prog_of_stripe=pg, stripe_of=sg)
+        if ev:
+            ev[1].record()
+
+    idx = torch.arange(S, device="cuda")
+    results = {}
+    for name, fn in (("partial_decoding", step_partial), ("fused", step_fused)):
+        rebuilt.zero_()
+        for _ in range(a.warmup):
+            fn()
+        torch.cuda.synchronize()
+        assert torch.equal(rebuilt[:, 0], stripes[idx, e_of.long()]), f"{name}: repair mismatch"
+        elapsed, evs = timed_loop(r, a.steps, fn)
+        t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+        n_local, n_glob = sl.numel(), sg.numel()
+        alg = (n_local * 7 + n_glob * 13) * B            # (survivors + 1) * B per repair
+        executed = alg if name == "fused" else (n_local * (4 + 4 + 3) + n_glob * 13) * B
+        results[name] = {"repairs_per_s": round(r.world * S * a.steps / elapsed, 1),
+                         "ms_per_batch": round(t * 1e3, 3),
+                         "algorithmic_GBps": round(alg / t / 1e9, 1),
+                         "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                         "executed_bytes_per_batch": executed}
+    return {"workload": "Azure-LRC(12,2,2) single-block repair, block s mod 16, 1 MiB", "n_gpus": r.world,
+            "stripes_per_gpu": S, "steps": a.steps, "results": results, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated on device)"}
+
+
+# ------------------------------------------------------------------------------- config 4
+
+def pc_merge(a, r):
+    """PC(4,1,4,1), 4 MiB blocks, merge x=2 HORIZONTAL: merged PC(8,1,4,1) row r parity = XOR of the
+    two old stripes' row-r data blocks (r < 4) / column-parity blocks (r = 4); the RS(8,1) row code is all
+    ones (main_recal / help_recal, handle_merge.cpp:159,269,319,453).  One launch reads 40 blocks and
+    writes 5 per merge (the algorithmic minimum, 9 * B per row)."""
+    B = a.block_size or (4 << 20)
+    S = a.stripes or 512
+    old = ecg.ec_factory(ecg.ECTYPE.PC, ecg.CodingParameters(k1=4, m1=1, k2=4, m2=1))
+    nb = old.k + old.m  # 25 blocks per PC(4,1,4,1) stripe
+    blocks = torch.empty((S, 2 * nb, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(blocks, 0xEC0DE, word_offset=D.data_word_offset(r.rank * S, 2 * nb, B))
+    # rowcol2bid (pc.cpp:326-340) of PC(4,1,4,1): data (r<4, c<4) = 4r + c; column parity (r=4, c<4) = 20 + c
+    def bid(row, col):
+        return row * 4 + col if row < 4 else 20 + col
+    src, coef = [], []
+    for row in range(5):
+        for half in range(2):
+            for col in range(4):
+                src.append(half * nb + bid(row, col))
+    for row in range(5):
+        coef.append([1 if j // 8 == row else 0 for j in range(40)])
+    out = torch.empty((S, 5, B), dtype=torch.uint8, device="cuda")
+    prog = [(coef, src, [0, 1, 2, 3, 4])]
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        ecg.matrix_apply_batch_multi(prog, blocks, out)
+        if ev:
+            ev[1].record()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    # check merges 0 and S-1 against XOR on the host
+    for s in (0, S - 1):
+        hb = blocks[s].cpu().numpy()
+        for row in range(5):
+            x = 0
+            for half in range(2):
+                for col in range(4):
+                    x = hb[half * nb + bid(row, col)] ^ x
+            assert (out[s, row].cpu().numpy() == x).all(), "merge mismatch"
+    elapsed, evs = timed_loop(r, a.steps, step)
+    t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+    alg = S * 45 * B
+    return {"workload": "PC(4,1,4,1) merge x=2 horizontal, 4 MiB blocks", "n_gpus": r.world,
+            "merges_per_gpu": S, "steps": a.steps, "ms_per_batch": round(t * 1e3, 3),
+            "merges_per_s": round(r.world * S * a.steps / elapsed, 1),
+            "algorithmic_GBps": round(alg / t / 1e9, 1), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+            "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
+
+
+# ------------------------------------------------------------------------------- config 5
+
+def rs4m_waves(a, r):
+    """RS(10,4), 4 MiB blocks, 65536 stripes sharded over the ranks; a rank's share (8192 stripes at N=8,
+    448 GiB) exceeds HBM, so it is encoded in resident waves of 1024 stripes (56 GiB); each wave's input
+    is regenerated on device outside the timed region."""
+    k, m = 10, 4
+    n = k + m
+    B = a.block_size or (4 << 20)
+    total = a.stripes or 65536
+    W = 1024
+    first, last = D.stripe_range(total, r)
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    wave = torch.empty((W, n, B), dtype=torch.uint8, device="cuda")
+    ev = events(1)[0]
+    kernel_s = 0.0
+    checks = 0
+    D.barrier(r)
+    torch.cuda.synchronize()
+    for s0 in range(first, last, W):
+        w = min(W, last - s0)
+        buf = wave[:w]
+        ecg.fill_random(buf, 0xEC0DE, word_offset=D.data_word_offset(s0, n, B))
+        ev[0].record()
+        ecg.encode_batch(k, m, M, buf[:, :k], buf[:, k:])
+        ev[1].record()
+        ev[1].synchronize()
+        kernel_s += ev[0].elapsed_time(ev[1]) / 1e3
+        checks = (checks + D.checksum64(buf[:, k:].contiguous())) & ((1 << 64) - 1)
+    t_max = D.max_over_ranks(kernel_s, r, device="cuda")
+    sums = D.gather_checksums(checks, r, device="cuda")
+    data_bytes = total * k * B
+    per_gpu = (last - first) * n * B / kernel_s / 1e9
+    return {"workload": f"RS(10,4) 4 MiB encode, {total} stripes over {r.world} GPU(s), waves of {W}",
+            "n_gpus": r.world, "aggregate_GiBps": round(data_bytes / t_max / 2 ** 30, 1),
+            "per_gpu_hbm_GBps_rank0": round(per_gpu, 1), "per_gpu_hbm_frac_rank0": round(per_gpu / HBM_PEAK_GBS, 4),
+            "encode_seconds_max": round(t_max, 3), "parity_checksum": f"{D.combine(sums):016x}",
+            "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
+
+
+def main():
+    a = parse()
+    r = D.from_env()
+    torch.cuda.set_device(r.local if r.distributed else 0)
+    D.init(r, "nccl", device=torch.device("cuda", r.local) if r.distributed else None)
+    ecg.lib().ecg_set_device(torch.cuda.current_device())
+    fn = {"rs-encode-decode": rs_encode_decode, "lrc-repair": lrc_repair, "pc-merge": pc_merge,
+          "rs4m-waves": rs4m_waves}[a.workload]
+    line = fn(a, r)
+    if r.rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if r.distributed:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

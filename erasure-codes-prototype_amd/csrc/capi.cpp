@@ -154,6 +154,25 @@ int ecg_matrix_apply_batch(int k_in, int m_out, const int* coef, const int* src_
                                           out_bstride, B, (hipStream_t)stream);
 }
 
+int ecg_matrix_apply_batch_multi(int n_prog, int k_in, int m_out, const int* coefs, const int* src_ids,
+                                 const int* dst_ids, const int* d_prog_of_stripe, const int* d_stripe_of,
+                                 const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
+                                 long long out_sstride, long long out_bstride, long long B, int S, void* stream) {
+    if (n_prog < 1 || k_in < 1 || m_out < 1 || !coefs || !src_ids || !dst_ids) return ECG_EINVAL;
+    if (n_prog > 1 && !d_prog_of_stripe) return ECG_EINVAL;
+    std::vector<LinearOp> progs(n_prog);
+    for (int p = 0; p < n_prog; p++) {
+        LinearOp& op = progs[p];
+        op.src_ids = vec(src_ids + (size_t)p * k_in, k_in);
+        op.dst_ids = vec(dst_ids + (size_t)p * m_out, m_out);
+        op.coef.resize((size_t)k_in * m_out);
+        const int* c = coefs + (size_t)p * k_in * m_out;
+        for (size_t i = 0; i < op.coef.size(); i++) op.coef[i] = (uint8_t)(c[i] & 0xff);
+    }
+    return Engine::instance().run_strided(progs, d_prog_of_stripe, S, in_base, in_sstride, in_bstride, out_base,
+                                          out_sstride, out_bstride, B, (hipStream_t)stream, d_stripe_of);
+}
+
 int ecg_encode_batch(int k, int m, const int* matrix, const void* d_in, long long in_sstride, long long in_bstride,
                      void* d_out, long long out_sstride, long long out_bstride, long long B, int S, void* stream) {
     if (k < 1 || m < 1 || !matrix) return ECG_EINVAL;

@@ -292,7 +292,8 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
 
 int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of_stripe, int S,
                         const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
-                        long long out_sstride, long long out_bstride, long long B, hipStream_t st) {
+                        long long out_sstride, long long out_bstride, long long B, hipStream_t st,
+                        const int* d_stripe_of) {
     if (S < 1 || B < 0 || !in_base || !out_base) return ECG_EINVAL;
     if (progs.size() > 1 && !d_prog_of_stripe) return ECG_EINVAL;
     int status = ECG_OK;
@@ -304,6 +305,7 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
     a.src_ids = ps->d_src;
     a.dst_ids = ps->d_dst;
     a.prog_of_stripe = progs.size() > 1 ? d_prog_of_stripe : nullptr;
+    a.stripe_of = d_stripe_of;
     a.in_base = (const uint8_t*)in_base;
     a.out_base = (uint8_t*)out_base;
     a.in_sstride = in_sstride;

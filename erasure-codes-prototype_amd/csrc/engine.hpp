@@ -43,7 +43,8 @@ public:
     int run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B);
     int run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of_stripe, int S,
                     const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
-                    long long out_sstride, long long out_bstride, long long B, hipStream_t stream);
+                    long long out_sstride, long long out_bstride, long long B, hipStream_t stream,
+                    const int* d_stripe_of = nullptr);
     int run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
                  bool aligned16, hipStream_t stream);
 

@@ -44,7 +44,8 @@ __device__ __forceinline__ const uint8_t* src_ptr(const GfLaunch& a, int s, int 
     } else if constexpr (MODE == GF_MODE_PTRS) {
         return cst(a.src_ptrs)[(size_t)s * a.k + j];
     } else {
-        return a.in_base + (long long)s * a.in_sstride + (long long)cst(a.src_ids)[prog * a.k + j] * a.in_bstride;
+        const long long sa = a.stripe_of ? (long long)cst(a.stripe_of)[s] : (long long)s;
+        return a.in_base + sa * a.in_sstride + (long long)cst(a.src_ids)[prog * a.k + j] * a.in_bstride;
     }
 }
 
@@ -55,7 +56,8 @@ __device__ __forceinline__ uint8_t* dst_ptr(const GfLaunch& a, int s, int prog, 
     } else if constexpr (MODE == GF_MODE_PTRS) {
         return cst(a.dst_ptrs)[(size_t)s * a.m + p];
     } else {
-        return a.out_base + (long long)s * a.out_sstride + (long long)cst(a.dst_ids)[prog * a.m + p] * a.out_bstride;
+        const long long sa = a.stripe_of ? (long long)cst(a.stripe_of)[s] : (long long)s;
+        return a.out_base + sa * a.out_sstride + (long long)cst(a.dst_ids)[prog * a.m + p] * a.out_bstride;
     }
 }
 

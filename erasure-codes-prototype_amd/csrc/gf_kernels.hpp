@@ -42,6 +42,7 @@ struct GfLaunch {
     const int* src_ids;
     const int* dst_ids;
     const int* prog_of_stripe;   // [S] or nullptr (program 0 for every stripe)
+    const int* stripe_of;        // [S] or nullptr: launch stripe i addresses stripe stripe_of[i] (STRIDED)
     // GF_MODE_STRIDED
     const uint8_t* in_base;
     uint8_t* out_base;

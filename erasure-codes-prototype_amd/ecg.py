@@ -46,7 +46,8 @@ EXPORTS = [
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
     "ecg_jerasure_invert_matrix", "ecg_jerasure_matrix_multiply", "ecg_galois_region_xor",
     "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode",
-    "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_encode_batch",
+    "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
+    "ecg_encode_batch",
     "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_fill_random",
     "ecg_ec_factory", "ecg_ec_destroy", "ecg_ec_init_coding_parameters", "ecg_ec_get_coding_parameters",
     "ecg_ec_set_memory", "ecg_ec_set_isvertical", "ecg_ec_k", "ecg_ec_m", "ecg_ec_make_encoding_matrix",
@@ -137,6 +138,7 @@ def lib():
         "ecg_dev_matrix_encode": ([I, I, IP, PP, PP, LL, P], I),
         "ecg_dev_matrix_decode": ([I, I, IP, I, IP, PP, PP, LL, P], I),
         "ecg_matrix_apply_batch": ([I, I, IP, IP, IP, P, LL, LL, P, LL, LL, LL, I, P], I),
+        "ecg_matrix_apply_batch_multi": ([I, I, I, IP, IP, IP, P, P, P, LL, LL, P, LL, LL, LL, I, P], I),
         "ecg_encode_batch": ([I, I, IP, P, LL, LL, P, LL, LL, LL, I, P], I),
         "ecg_decode_batch": ([I, I, IP, I, IP, I, P, P, LL, LL, P, LL, LL, LL, I, P], I),
         "ecg_perform_addition_batch": ([I, I, P, LL, LL, P, LL, LL, LL, I, P], I),
@@ -313,6 +315,29 @@ def matrix_apply_batch(coef, src_ids, dst_ids, d_in, d_out, stream=None):
     return _check(lib().ecg_matrix_apply_batch(len(src_ids), len(dst_ids), _ints(coef.ravel()), _ints(src_ids),
                                                _ints(dst_ids), d_in.data_ptr(), iss, ibs, d_out.data_ptr(), oss, obs,
                                                B, S, _stream(stream)), "matrix_apply_batch")
+
+
+def matrix_apply_batch_multi(programs, d_in, d_out, prog_of_stripe=None, stripe_of=None, n_launch=None,
+                             stream=None):
+    """programs: list of (coef [n_out][n_in], src_ids, dst_ids), all of the same shape.  Launch stripe
+    i runs programs[prog_of_stripe[i]] on stripe stripe_of[i] (int32 CUDA tensors; None = identity)."""
+    n_prog = len(programs)
+    k_in, m_out = len(programs[0][1]), len(programs[0][2])
+    coefs, srcs, dsts = [], [], []
+    for coef, src, dst in programs:
+        c = np.asarray(coef, dtype=np.int64).reshape(m_out, k_in)
+        coefs += list(c.ravel())
+        srcs += list(src)
+        dsts += list(dst)
+    _, _, B = d_in.shape
+    S = n_launch if n_launch is not None else (stripe_of.numel() if stripe_of is not None else d_in.shape[0])
+    iss, ibs = _strides(d_in)
+    oss, obs = _strides(d_out)
+    return _check(lib().ecg_matrix_apply_batch_multi(
+        n_prog, k_in, m_out, _ints(coefs), _ints(srcs), _ints(dsts),
+        prog_of_stripe.data_ptr() if prog_of_stripe is not None else None,
+        stripe_of.data_ptr() if stripe_of is not None else None,
+        d_in.data_ptr(), iss, ibs, d_out.data_ptr(), oss, obs, B, S, _stream(stream)), "matrix_apply_batch_multi")
 
 
 def perform_addition_batch(block_num, parity_num, d_in, d_out, stream=None):

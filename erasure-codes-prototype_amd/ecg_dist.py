@@ -1,0 +1,96 @@
+"""Stripe sharding across GPUs: one process per GPU, no data-path collective.
+
+Stripes are independent (the proxy loops stripes with no cross-stripe state, proxy.cpp:312-399), so a
+batch of S_total stripes is partitioned into contiguous ranges, one per rank.  torch.distributed is
+used only around the data path: a barrier before/after the timed region, a MAX of elapsed times, a SUM
+of processed bytes and an all-gather of per-rank 64-bit parity checksums for a bit-exact verdict.
+Backend "nccl" (RCCL over xGMI) on GPUs, "gloo" in CPU tests.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+_MASK64 = (1 << 64) - 1
+
+
+@dataclass
+class Rank:
+    rank: int
+    world: int
+    local: int
+
+    @property
+    def distributed(self):
+        return self.world > 1
+
+
+def from_env() -> Rank:
+    return Rank(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+                int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(r: Rank, backend: str = "nccl", device=None) -> None:
+    if r.distributed and not dist.is_initialized():
+        if device is not None:
+            dist.init_process_group(backend, device_id=device)
+        else:
+            dist.init_process_group(backend)
+
+
+def stripe_range(total: int, r: Rank) -> tuple[int, int]:
+    """Contiguous [first, last) stripes of rank r; sizes differ by at most one."""
+    base, extra = divmod(total, r.world)
+    first = r.rank * base + min(r.rank, extra)
+    return first, first + base + (1 if r.rank < extra else 0)
+
+
+def data_word_offset(first_stripe: int, n_blocks: int, block_size: int) -> int:
+    """splitmix64 word offset of a rank's first stripe, so every rank generates the bytes the global
+    batch would hold (a stripe's bytes do not depend on how the batch is sharded)."""
+    return first_stripe * n_blocks * block_size // 8
+
+
+def barrier(r: Rank) -> None:
+    if r.distributed:
+        dist.barrier()
+
+
+def _reduce(value: float, r: Rank, op, device) -> float:
+    if not r.distributed:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
+def max_over_ranks(value: float, r: Rank, device="cpu") -> float:
+    return _reduce(value, r, dist.ReduceOp.MAX, device)
+
+
+def sum_over_ranks(value: float, r: Rank, device="cpu") -> float:
+    return _reduce(value, r, dist.ReduceOp.SUM, device)
+
+
+def checksum64(t: torch.Tensor) -> int:
+    """Order-independent 64-bit checksum of a uint8 buffer: sum of its little-endian 8-byte words mod
+    2^64 (the buffer length must be a multiple of 8)."""
+    words = t.reshape(-1).view(torch.int64)
+    return int(words.sum().item()) & _MASK64
+
+
+def combine(checksums) -> int:
+    return sum(int(c) for c in checksums) & _MASK64
+
+
+def gather_checksums(c: int, r: Rank, device="cpu") -> list[int]:
+    if not r.distributed:
+        return [c]
+    v = c if c < (1 << 63) else c - (1 << 64)  # carry the 64-bit pattern in a signed tensor
+    t = torch.tensor([v], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(r.world)]
+    dist.all_gather(out, t)
+    return [int(x.item()) & _MASK64 for x in out]

@@ -85,6 +85,14 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
 int ecg_matrix_apply_batch(int k_in, int m_out, const int* coef, const int* src_ids, const int* dst_ids,
                            const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
                            long long out_sstride, long long out_bstride, long long B, int S, void* stream);
+/* Several programs in one launch (all k_in x m_out): launch stripe i runs program d_prog_of_stripe[i]
+ * (device int[S]; NULL if n_prog == 1) on stripe d_stripe_of[i] (device int[S]; NULL = i) of the
+ * strided layout.  coefs: n_prog x m_out x k_in; src_ids: n_prog x k_in; dst_ids: n_prog x m_out.
+ * Used for rotating repair patterns (config 3) and for launching over a subset of a batch. */
+int ecg_matrix_apply_batch_multi(int n_prog, int k_in, int m_out, const int* coefs, const int* src_ids,
+                                 const int* dst_ids, const int* d_prog_of_stripe, const int* d_stripe_of,
+                                 const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
+                                 long long out_sstride, long long out_bstride, long long B, int S, void* stream);
 /* Batched jerasure_matrix_encode: in [S] x k blocks, out [S] x m blocks (coding block i at index i). */
 int ecg_encode_batch(int k, int m, const int* matrix, const void* d_in, long long in_sstride, long long in_bstride,
                      void* d_out, long long out_sstride, long long out_bstride, long long B, int S, void* stream);

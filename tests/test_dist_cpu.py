@@ -1,0 +1,89 @@
+"""N>1 path on CPU: world_size-2 gloo processes run ecg_dist's sharding, barrier, max-reduce and
+checksum all-gather exactly as bench.py does on GPUs.  The per-stripe coding work is done by the oracle
+(CPU stand-in: this test covers the distributed logic, the kernels are covered by the GPU tests)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _encode_range(first, last, k, m, B, seed):
+    from oracle import ref
+    M = ref.reed_sol_vandermonde_coding_matrix(k, m)
+    out = []
+    for s in range(first, last):
+        data = [ref.splitmix_bytes(seed, (s * (k + m) + j) * B // 8, B) for j in range(k)]
+        coding = [np.zeros(B, np.uint8) for _ in range(m)]
+        ref.jerasure_matrix_encode(k, m, M, data, coding, B)
+        out.append(np.concatenate(coding))
+    return np.concatenate(out) if out else np.zeros(0, np.uint8)
+
+
+def _worker(rank, world, port, total, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import ecg_dist as D
+    r = D.from_env()
+    D.init(r, backend="gloo")
+    k, m, B, seed = 6, 3, 256, 0xEC0DE
+    first, last = D.stripe_range(total, r)
+    D.barrier(r)
+    par = _encode_range(first, last, k, m, B, seed)
+    c = D.checksum64(torch.from_numpy(par))
+    sums = D.gather_checksums(c, r)
+    t = D.max_over_ranks(float(rank + 1), r)
+    n = D.sum_over_ranks(float(last - first), r)
+    D.barrier(r)
+    q.put((rank, first, last, sums, t, n))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [10, 3])
+def test_two_rank_sharding_matches_single_process(total):
+    sys.path[:0] = [os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    import ecg_dist as D
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    [p.start() for p in procs]
+    res = sorted(q.get(timeout=120) for _ in procs)
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    # ranges tile [0, total) contiguously
+    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == total
+    # every rank saw the same gathered checksums; combined == single-process checksum
+    assert res[0][3] == res[1][3]
+    full = _encode_range(0, total, 6, 3, 256, 0xEC0DE)
+    assert D.combine(res[0][3]) == D.checksum64(torch.from_numpy(full))
+    # max over ranks of (rank+1) and the sum of processed stripes
+    assert res[0][4] == res[1][4] == 2.0
+    assert res[0][5] == res[1][5] == float(total)
+
+
+def test_stripe_range_single_and_uneven():
+    sys.path[:0] = [os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    import ecg_dist as D
+    for total in (0, 1, 7, 8, 65536):
+        for world in (1, 2, 3, 8):
+            spans = [D.stripe_range(total, D.Rank(r, world, r)) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+    assert D.data_word_offset(3, 14, 1 << 20) == 3 * 14 * (1 << 20) // 8

@@ -423,3 +423,33 @@ def test_full_size_rs10_4_round_trip(ecg, oracle, torch_cuda):
         assert same([h[k + i] for i in range(m)], ref), s
     del stripes, out, expect
     torch.cuda.empty_cache()
+
+
+def test_matrix_apply_multi_with_stripe_subset(ecg, oracle, torch_cuda):
+    """Several programs per launch + launch over a subset of the batch (stripe_of indirection)."""
+    torch = torch_cuda
+    rng = random.Random(11)
+    S, n, B = 24, 8, 4096 + 16
+    d_in = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(d_in, 21)
+    out = torch.zeros((S, 2, B), dtype=torch.uint8, device="cuda")
+    progs = []
+    for _ in range(5):
+        src = rng.sample(range(n), 3)
+        coef = [[rng.randrange(256) for _ in range(3)] for _ in range(2)]
+        progs.append((coef, src, [1, 0]))
+    subset = sorted(rng.sample(range(S), 11))
+    which = [rng.randrange(5) for _ in subset]
+    st = torch.tensor(subset, dtype=torch.int32, device="cuda")
+    pp = torch.tensor(which, dtype=torch.int32, device="cuda")
+    ecg.matrix_apply_batch_multi(progs, d_in, out, prog_of_stripe=pp, stripe_of=st)
+    torch.cuda.synchronize()
+    hin, hout = d_in.cpu().numpy(), out.cpu().numpy()
+    for s in range(S):
+        if s not in subset:
+            assert not hout[s].any(), s
+            continue
+        coef, src, dst = progs[which[subset.index(s)]]
+        ref = [np.zeros(B, np.uint8) for _ in range(2)]
+        oracle.jerasure_matrix_encode(3, 2, [c for r in coef for c in r], [hin[s, j] for j in src], ref, B)
+        assert np.array_equal(hout[s, 1], ref[0]) and np.array_equal(hout[s, 0], ref[1]), s
