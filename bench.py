@@ -17,7 +17,9 @@ Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line
   pc-merge    configs[3]: PC(4,1,4,1), 4 MiB blocks, stripe merging x=2 (HORIZONTAL): the 5 row
               parities of the merged PC(8,1,4,1) recomputed from the two old stripes;
   rs4m-waves  configs[4]: RS(10,4), 4 MiB blocks, 65536 stripes split over the ranks, encoded in
-              HBM-resident waves of 1024 stripes (input regenerated per wave outside the timing).
+              HBM-resident waves of 1024 stripes (input regenerated per wave outside the timing);
+  rs-host     configs[1] with the blocks in pinned HOST memory: the rate including hipMemcpyAsync to and
+              from the GPU over PCIe (H2D -> kernel -> D2H pipeline), for DESIGN.md.
 
 Multi-GPU: one process per GPU (torch.distributed.run), stripes sharded per rank (ecg_dist), no
 data-path collective: barrier + synchronize around the timed region, elapsed time max-reduced,
@@ -49,7 +51,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs-encode-decode",
-                    choices=["rs-encode-decode", "lrc-repair", "pc-merge", "rs4m-waves"])
+                    choices=["rs-encode-decode", "lrc-repair", "pc-merge", "rs4m-waves", "rs-host"])
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -390,6 +392,43 @@ def rs4m_waves(a, r):
             "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
+# ------------------------------------------------------------------------------- host-resident
+
+def rs_host(a, r):
+    """RS(10,4), 1 MiB, host-resident (pinned) batch: encode and single-erasure decode including the
+    PCIe copies (ecg_encode_batch_host / ecg_decode_batch_host pipelines), chunk size swept."""
+    k, m = 10, 4
+    n = k + m
+    B = a.block_size or (1 << 20)
+    S = a.stripes or 512
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    stripes = torch.empty((S, n, B), dtype=torch.uint8).pin_memory()
+    dev = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(dev, 0xEC0DE, word_offset=D.data_word_offset(r.rank * S, n, B))
+    stripes.copy_(dev)
+    del dev
+    torch.cuda.empty_cache()
+    out = torch.empty((S, 1, B), dtype=torch.uint8).pin_memory()
+    res = {}
+    for chunk in (4, 16, 64):
+        for name, fn, nbytes in (
+                ("encode", lambda: ecg.encode_batch_host(k, m, M, stripes[:, :k], stripes[:, k:], chunk), S * k * B),
+                ("decode", lambda: ecg.decode_batch_host(k, m, M, 1, [3], stripes, h_out=out, chunk_stripes=chunk),
+                 S * k * B)):
+            fn()
+            ts = []
+            for _ in range(max(2, a.steps // 3)):
+                D.barrier(r)
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            t = D.max_over_ranks(min(ts), r, device="cuda")
+            res[f"{name}_chunk{chunk}_GiBps"] = round(r.world * nbytes / t / 2 ** 30, 2)
+    return {"workload": f"RS(10,4) 1 MiB, {S} stripes in pinned host memory, incl. PCIe H2D/D2H",
+            "n_gpus": r.world, "results": res, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated on device, copied to pinned host buffers)"}
+
+
 def main():
     a = parse()
     r = D.from_env()
@@ -397,7 +436,7 @@ def main():
     D.init(r, "nccl", device=torch.device("cuda", r.local) if r.distributed else None)
     ecg.lib().ecg_set_device(torch.cuda.current_device())
     fn = {"rs-encode-decode": rs_encode_decode, "lrc-repair": lrc_repair, "pc-merge": pc_merge,
-          "rs4m-waves": rs4m_waves}[a.workload]
+          "rs4m-waves": rs4m_waves, "rs-host": rs_host}[a.workload]
     line = fn(a, r)
     if r.rank == 0:
         print(json.dumps(line), flush=True)

@@ -208,6 +208,32 @@ int ecg_decode_batch(int k, int m, const int* matrix, int row_k_ones, const int*
                                           (hipStream_t)stream);
 }
 
+int ecg_encode_batch_host(int k, int m, const int* matrix, const void* h_in, long long in_sstride,
+                          long long in_bstride, void* h_out, long long out_sstride, long long out_bstride, long long B,
+                          int S, int chunk_stripes) {
+    if (k < 1 || m < 1 || !matrix) return ECG_EINVAL;
+    LinearOp op = plan_matrix_encode(k, m, matrix);
+    if (op.m_out() == 0) return ECG_OK;
+    for (int& d : op.dst_ids) d -= k;
+    return Engine::instance().run_host_pipeline(op, h_in, in_sstride, in_bstride, h_out, out_sstride, out_bstride, B,
+                                                S, chunk_stripes);
+}
+
+int ecg_decode_batch_host(int k, int m, const int* matrix, int row_k_ones, const int* erasures, void* h_stripes,
+                          long long sstride, long long bstride, void* h_out, long long out_sstride,
+                          long long out_bstride, long long B, int S, int chunk_stripes) {
+    if (k < 1 || m < 1 || !matrix || !erasures) return ECG_EINVAL;
+    std::vector<LinearOp> ops;
+    if (plan_matrix_decode(k, m, matrix, row_k_ones, erasures, ops) < 0) return ECG_EUNDECODABLE;
+    if (ops.empty()) return ECG_OK;
+    if (ops.size() != 1) return ECG_EINVAL;
+    if (h_out)
+        for (size_t i = 0; i < ops[0].dst_ids.size(); i++) ops[0].dst_ids[i] = (int)i;
+    return Engine::instance().run_host_pipeline(ops[0], h_stripes, sstride, bstride, h_out ? h_out : h_stripes,
+                                                h_out ? out_sstride : sstride, h_out ? out_bstride : bstride, B, S,
+                                                chunk_stripes);
+}
+
 int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, long long in_sstride,
                                long long in_bstride, void* d_out, long long out_sstride, long long out_bstride,
                                long long B, int S, void* stream) {

@@ -34,6 +34,12 @@ struct ThreadCtx {
     size_t cap = 0;
     void** d_ptrs = nullptr;     // pointer tables for ops too wide for kernel arguments
     size_t d_ptrs_cap = 0;
+    // host-batch pipeline: 3 streams, 3 device slots
+    hipStream_t pstream[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t in_done[3] = {}, comp_done[3] = {}, out_done[3] = {};
+    bool pipe_ready = false;
+    uint8_t* pslot = nullptr;
+    size_t pslot_cap = 0;
     ~ThreadCtx() {
         // Process teardown may already have destroyed the runtime; leak rather than fault.
     }
@@ -346,6 +352,89 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
     a.rtiles = ps->rtiles;
     a.binary = ps->binary ? 1 : 0;
     ECG_HIP(launch_gf(a, GF_MODE_PTRS, aligned, st));
+    return ECG_OK;
+}
+
+int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long in_sstride, long long in_bstride,
+                              void* h_out, long long out_sstride, long long out_bstride, long long B, int S,
+                              int chunk) {
+    if (S < 1 || B < 1 || !h_in || !h_out || prog.k_in() < 1 || prog.m_out() < 1) return ECG_EINVAL;
+    if (chunk < 1) chunk = 16;
+    if (chunk > S) chunk = S;
+    const int kin = prog.k_in(), mout = prog.m_out();
+    const size_t pitch = ((size_t)B + 255) & ~(size_t)255;
+    const size_t slot_in = (size_t)chunk * kin * pitch, slot_out = (size_t)chunk * mout * pitch;
+    ThreadCtx& c = tctx(device_);
+    if (!c.pipe_ready) {
+        for (int i = 0; i < 3; i++) {
+            ECG_HIP(hipStreamCreateWithFlags(&c.pstream[i], hipStreamNonBlocking));
+            ECG_HIP(hipEventCreateWithFlags(&c.in_done[i], hipEventDisableTiming));
+            ECG_HIP(hipEventCreateWithFlags(&c.comp_done[i], hipEventDisableTiming));
+            ECG_HIP(hipEventCreateWithFlags(&c.out_done[i], hipEventDisableTiming));
+        }
+        c.pipe_ready = true;
+    }
+    if (c.pslot_cap < 3 * (slot_in + slot_out)) {
+        for (int i = 0; i < 3; i++) ECG_HIP(hipStreamSynchronize(c.pstream[i]));
+        if (c.pslot) (void)hipFree(c.pslot);
+        c.pslot = nullptr;
+        c.pslot_cap = 0;
+        ECG_HIP(hipMalloc(&c.pslot, 3 * (slot_in + slot_out)));
+        c.pslot_cap = 3 * (slot_in + slot_out);
+    }
+    // the device program reads compact slot blocks 0..kin-1 and writes 0..mout-1
+    LinearOp dev = prog;
+    for (int j = 0; j < kin; j++) dev.src_ids[j] = j;
+    for (int p = 0; p < mout; p++) dev.dst_ids[p] = p;
+    int status = ECG_OK;
+    std::shared_ptr<ProgramSet> ps = program_set({dev}, &status);
+    if (!ps) return status;
+    hipStream_t s_in = c.pstream[0], s_comp = c.pstream[1], s_out = c.pstream[2];
+    const uint8_t* hin = (const uint8_t*)h_in;
+    uint8_t* hout = (uint8_t*)h_out;
+    bool used[3] = {false, false, false};
+    for (int s0 = 0, it = 0; s0 < S; s0 += chunk, it++) {
+        const int n = std::min(chunk, S - s0);
+        const int slot = it % 3;
+        uint8_t* din = c.pslot + (size_t)slot * (slot_in + slot_out);
+        uint8_t* dout = din + slot_in;
+        if (used[slot]) ECG_HIP(hipStreamWaitEvent(s_in, c.comp_done[slot], 0));  // slot's inputs consumed
+        for (int j = 0; j < kin; j++)
+            ECG_HIP(hipMemcpy2DAsync(din + (size_t)j * pitch, (size_t)kin * pitch,
+                                     hin + (size_t)s0 * in_sstride + (size_t)prog.src_ids[j] * in_bstride,
+                                     (size_t)in_sstride, (size_t)B, (size_t)n, hipMemcpyHostToDevice, s_in));
+        ECG_HIP(hipEventRecord(c.in_done[slot], s_in));
+        ECG_HIP(hipStreamWaitEvent(s_comp, c.in_done[slot], 0));
+        if (used[slot]) ECG_HIP(hipStreamWaitEvent(s_comp, c.out_done[slot], 0));  // slot's outputs copied out
+        GfLaunch a;
+        memset(&a, 0, sizeof(a));
+        a.tabs = ps->d_tabs;
+        a.src_ids = ps->d_src;
+        a.dst_ids = ps->d_dst;
+        a.in_base = din;
+        a.out_base = dout;
+        a.in_sstride = (long long)(kin * pitch);
+        a.in_bstride = (long long)pitch;
+        a.out_sstride = (long long)(mout * pitch);
+        a.out_bstride = (long long)pitch;
+        a.B = B;
+        a.k = ps->k;
+        a.m = ps->m;
+        a.S = n;
+        a.MT = ps->MT;
+        a.rtiles = ps->rtiles;
+        a.binary = ps->binary ? 1 : 0;
+        ECG_HIP(launch_gf(a, GF_MODE_STRIDED, true, s_comp));
+        ECG_HIP(hipEventRecord(c.comp_done[slot], s_comp));
+        ECG_HIP(hipStreamWaitEvent(s_out, c.comp_done[slot], 0));
+        for (int p = 0; p < mout; p++)
+            ECG_HIP(hipMemcpy2DAsync(hout + (size_t)s0 * out_sstride + (size_t)prog.dst_ids[p] * out_bstride,
+                                     (size_t)out_sstride, dout + (size_t)p * pitch, (size_t)mout * pitch, (size_t)B,
+                                     (size_t)n, hipMemcpyDeviceToHost, s_out));
+        ECG_HIP(hipEventRecord(c.out_done[slot], s_out));
+        used[slot] = true;
+    }
+    ECG_HIP(hipStreamSynchronize(s_out));
     return ECG_OK;
 }
 

@@ -1,6 +1,6 @@
 // GF(2^8) region engine: turns LinearOps (matrix.hpp) into HIP launches on gfx950.
 //
-// Three ways in:
+// Four ways in (plus run_host_pipeline for host-resident batches):
 //   run_device  - block pointers are device pointers (HBM-resident), asynchronous on a stream;
 //   run_host    - block pointers are host buffers (the reference's char** of host memory): blocks are
 //                 staged into per-thread device scratch, each block copied in at most once and every
@@ -47,6 +47,13 @@ public:
                     const int* d_stripe_of = nullptr);
     int run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
                  bool aligned16, hipStream_t stream);
+
+    // Host-resident batch (block b of stripe s at h_in + s*in_sstride + b*in_bstride, likewise out):
+    // a 3-slot pipeline of H2D (2-D copies of the blocks the program reads), kernel, D2H (the blocks
+    // it writes) on three streams, chunk_stripes stripes per slot.  Synchronous.
+    int run_host_pipeline(const LinearOp& prog, const void* h_in, long long in_sstride, long long in_bstride,
+                          void* h_out, long long out_sstride, long long out_bstride, long long B, int S,
+                          int chunk_stripes);
 
     std::shared_ptr<ProgramSet> program_set(const std::vector<LinearOp>& progs, int* status);
     hipStream_t thread_stream();  // per-thread non-blocking stream used by the host tier

@@ -34,7 +34,10 @@ enum GfMode : int {
 constexpr int kInlineSrc = 128;
 constexpr int kInlineDst = 32;
 constexpr int kMaxMT = 8;       // output rows per row tile
-constexpr int kThreads = 256;   // 4 waves of 64
+#ifndef ECG_TPB
+#define ECG_TPB 256
+#endif
+constexpr int kThreads = ECG_TPB;  // threads per workgroup (4 waves of 64); ECG_TPB only for tuning builds
 
 struct GfLaunch {
     // programs: [nprog][rtiles][k][MT] tables, [nprog][k] src ids, [nprog][m] dst ids

@@ -25,7 +25,7 @@ except Exception:  # pragma: no cover - torch is optional for host-tier use
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libecg.so")
+LIB_PATH = os.environ.get("ECG_LIB") or os.path.join(_HERE, "lib", "libecg.so")  # ECG_LIB: tuning builds only
 
 ECG_OK = 0
 ECG_EUNDECODABLE = -1
@@ -48,7 +48,8 @@ EXPORTS = [
     "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode",
     "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
     "ecg_encode_batch",
-    "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_fill_random",
+    "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
+    "ecg_fill_random",
     "ecg_ec_factory", "ecg_ec_destroy", "ecg_ec_init_coding_parameters", "ecg_ec_get_coding_parameters",
     "ecg_ec_set_memory", "ecg_ec_set_isvertical", "ecg_ec_k", "ecg_ec_m", "ecg_ec_make_encoding_matrix",
     "ecg_ec_check_if_decodable", "ecg_ec_encode", "ecg_ec_decode",
@@ -142,6 +143,8 @@ def lib():
         "ecg_encode_batch": ([I, I, IP, P, LL, LL, P, LL, LL, LL, I, P], I),
         "ecg_decode_batch": ([I, I, IP, I, IP, I, P, P, LL, LL, P, LL, LL, LL, I, P], I),
         "ecg_perform_addition_batch": ([I, I, P, LL, LL, P, LL, LL, LL, I, P], I),
+        "ecg_encode_batch_host": ([I, I, IP, P, LL, LL, P, LL, LL, LL, I, I], I),
+        "ecg_decode_batch_host": ([I, I, IP, I, IP, P, LL, LL, P, LL, LL, LL, I, I], I),
         "ecg_fill_random": ([P, LL, ULL, ULL, P], I),
         "ecg_ec_factory": ([I, ctypes.POINTER(_CP)], P),
         "ecg_ec_destroy": ([P], None),
@@ -346,6 +349,31 @@ def perform_addition_batch(block_num, parity_num, d_in, d_out, stream=None):
     oss, obs = _strides(d_out)
     return _check(lib().ecg_perform_addition_batch(block_num, parity_num, d_in.data_ptr(), iss, ibs, d_out.data_ptr(),
                                                    oss, obs, B, S, _stream(stream)), "perform_addition_batch")
+
+
+def _host_strides(a):
+    """(stripe stride, block stride) in bytes of a [S][n][B] host array (numpy or pinned torch CPU)."""
+    if isinstance(a, np.ndarray):
+        return a.strides[0], a.strides[1], a.ctypes.data
+    return a.stride(0), a.stride(1), a.data_ptr()
+
+
+def encode_batch_host(k, m, matrix, h_in, h_out, chunk_stripes=0):
+    """Host-resident RS/any-matrix encode through the H2D -> kernel -> D2H pipeline.  h_in [S][k][B],
+    h_out [S][m][B] (numpy or pinned torch CPU uint8)."""
+    S, _, B = h_in.shape
+    iss, ibs, ip = _host_strides(h_in)
+    oss, obs, op = _host_strides(h_out)
+    return _check(lib().ecg_encode_batch_host(k, m, _ints(matrix), ip, iss, ibs, op, oss, obs, B, S, chunk_stripes),
+                  "encode_batch_host")
+
+
+def decode_batch_host(k, m, matrix, row_k_ones, erasures, h_stripes, h_out=None, chunk_stripes=0):
+    S, _, B = h_stripes.shape
+    ss, bs, sp = _host_strides(h_stripes)
+    oss, obs, op = _host_strides(h_out) if h_out is not None else (0, 0, None)
+    return _check(lib().ecg_decode_batch_host(k, m, _ints(matrix), int(bool(row_k_ones)), _ints(list(erasures) + [-1]),
+                                              sp, ss, bs, op, oss, obs, B, S, chunk_stripes), "decode_batch_host")
 
 
 def fill_random(t, seed, word_offset=0, stream=None):

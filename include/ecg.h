@@ -108,6 +108,18 @@ int ecg_decode_batch(int k, int m, const int* matrix, int row_k_ones, const int*
 int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, long long in_sstride,
                                long long in_bstride, void* d_out, long long out_sstride, long long out_bstride,
                                long long B, int S, void* stream);
+/* Host-resident batches (the path starts and ends in host memory: proxy sockets / datanode buffers).
+ * Same layouts as above but HOST pointers (pin them -- hipHostMalloc / hipHostRegister -- for full PCIe
+ * rate).  Chunks of chunk_stripes stripes (0 = 16) flow through a 3-stage pipeline: H2D of the blocks
+ * the program reads, kernel, D2H of the blocks it writes, on three streams so the three overlap.
+ * Synchronous: returns when every output byte is in host memory. */
+int ecg_encode_batch_host(int k, int m, const int* matrix, const void* h_in, long long in_sstride,
+                          long long in_bstride, void* h_out, long long out_sstride, long long out_bstride, long long B,
+                          int S, int chunk_stripes);
+/* One erasure pattern for every stripe; h_out == NULL writes the rebuilt blocks in place. */
+int ecg_decode_batch_host(int k, int m, const int* matrix, int row_k_ones, const int* erasures, void* h_stripes,
+                          long long sstride, long long bstride, void* h_out, long long out_sstride,
+                          long long out_bstride, long long B, int S, int chunk_stripes);
 /* Deterministic synthetic bytes (splitmix64 counter). */
 int ecg_fill_random(void* d_dst, long long nbytes, unsigned long long seed, unsigned long long word_offset,
                     void* stream);

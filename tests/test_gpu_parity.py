@@ -453,3 +453,33 @@ def test_matrix_apply_multi_with_stripe_subset(ecg, oracle, torch_cuda):
         ref = [np.zeros(B, np.uint8) for _ in range(2)]
         oracle.jerasure_matrix_encode(3, 2, [c for r in coef for c in r], [hin[s, j] for j in src], ref, B)
         assert np.array_equal(hout[s, 1], ref[0]) and np.array_equal(hout[s, 0], ref[1]), s
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline_encode_decode(ecg, oracle, torch_cuda, pinned):
+    """Host-resident batches through the H2D -> kernel -> D2H pipeline (chunks not dividing S)."""
+    torch = torch_cuda
+    k, m, B, S = 10, 4, 65536 + 48, 11
+    n = k + m
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    if pinned:
+        stripes = torch.empty((S, n, B), dtype=torch.uint8).pin_memory()
+        stripes.numpy()[:] = np.frombuffer(oracle.splitmix_bytes(4, 0, S * n * B), np.uint8).reshape(S, n, B)
+        h = stripes.numpy()
+    else:
+        h = oracle.splitmix_bytes(4, 0, S * n * B).reshape(S, n, B).copy()
+        stripes = h
+    data_view = stripes[:, :k]
+    coding_view = stripes[:, k:]
+    ecg.encode_batch_host(k, m, M, data_view, coding_view, chunk_stripes=4)
+    for s in range(S):
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode(k, m, M, [h[s, j].copy() for j in range(k)], ref, B)
+        assert same([h[s, k + i] for i in range(m)], ref), s
+    orig = h.copy()
+    out = np.zeros((S, 2, B), np.uint8)
+    ecg.decode_batch_host(k, m, M, 1, [2, 12], stripes, h_out=out, chunk_stripes=3)
+    assert np.array_equal(out[:, 0], orig[:, 2]) and np.array_equal(out[:, 1], orig[:, 12])
+    h[:, 5] = 0
+    ecg.decode_batch_host(k, m, M, 1, [5], stripes, chunk_stripes=5)  # in place
+    assert np.array_equal(h, orig)
