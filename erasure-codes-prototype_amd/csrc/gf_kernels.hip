@@ -155,7 +155,8 @@ constexpr int occupancy_for(int MT) { return MT <= 4 ? 6 : 4; }
 // Workgroup -> (stripe, column chunk).  grid_map 0: linear (workgroup b takes chunk b).  grid_map 1:
 // XCD-contiguous -- the dispatcher deals workgroups round-robin over the 8 XCDs, so b % 8 names the
 // XCD group; each group is given a contiguous 1/8 of the chunk list (T1 in the HIP guide; here for
-// DRAM locality of the concurrently active chunks, not L2 reuse).  Speed only, never correctness.
+// DRAM locality of the concurrently active chunks, not L2 reuse).  grid_map 2: launch stripe s runs on
+// XCD group s % 8, chunks of a stripe in order.  Speed only, never correctness.
 __device__ __forceinline__ void wg_coords(const GfLaunch& a, int& s, int& w) {
     long long b = blockIdx.x;
     if (a.grid_map == 1) {
@@ -294,7 +295,7 @@ void init_options() {
     };
     g_opt[ECG_OPT_NT].store(env("ECG_NT", 3));
     g_opt[ECG_OPT_COLS_PER_WG].store(env("ECG_COLS_PER_WG", 0));
-    g_opt[ECG_OPT_GRID_MAP].store(env("ECG_GRID_MAP", 1));
+    g_opt[ECG_OPT_GRID_MAP].store(env("ECG_GRID_MAP", 3));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -374,8 +375,19 @@ int set_option(int opt, long long value) {
     if (opt < 0 || opt >= ECG_OPT_COUNT) return -1;
     if (opt == ECG_OPT_NT && (value < 0 || value > 3)) return -1;
     if (opt == ECG_OPT_COLS_PER_WG && (value < 0 || (value % kThreads) != 0)) return -1;
+    if (opt == ECG_OPT_GRID_MAP && (value < 0 || value > 3)) return -1;
     g_opt[opt].store(value);
     return 0;
+}
+
+// Grid-map auto rule (r01 tools/shape_sweep.py, every k_in x m_out shape): when the outputs are blocks
+// of the input stripes themselves (encode: [S][k+m][B]), XCD-contiguous chunks (map 1) are 1-3 % faster;
+// when they go to a separate buffer (decode / repair / merge outputs), putting stripe s on XCD s % 8
+// (map 2) is 2-6 % faster.  Pointer-table launches have no single layout and take map 1.
+static bool outputs_in_stripe(const GfLaunch& a, int mode) {
+    if (mode != GF_MODE_STRIDED) return true;
+    const uint8_t* o = a.out_base;
+    return a.out_sstride == a.in_sstride && o >= a.in_base && o < a.in_base + a.in_sstride;
 }
 
 hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st) {
@@ -390,15 +402,17 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
     if (vec_bytes > 0) {
         const long long ncols = vec_bytes >> 4;
         long long cpw = g_opt[ECG_OPT_COLS_PER_WG].load();
-        if (cpw <= 0) cpw = kThreads;  // 4 KiB of every block per workgroup (measured best, r01 microbench)
+        if (cpw <= 0) cpw = kThreads;  // 2 KiB of every block per workgroup (measured best, r01 microbench)
         if (ncols < cpw) cpw = ((ncols + kThreads - 1) / kThreads) * kThreads;
         a.cols_per_wg = (int)cpw;
         a.wg_per_stripe = (int)((ncols + cpw - 1) / cpw);
         a.off0 = 0;
         const long long gx = (long long)a.S * a.wg_per_stripe;
         if (gx > 0x7fffffffLL) return hipErrorInvalidConfiguration;
-        const long long gm = g_opt[ECG_OPT_GRID_MAP].load();
-        a.grid_map = (gm == 1 && gx % 8 == 0) ? 1 : (gm == 2 && a.S % 8 == 0) ? 2 : 0;
+        long long gm = g_opt[ECG_OPT_GRID_MAP].load();
+        if (gm == 3) gm = outputs_in_stripe(a, mode) ? 1 : 2;
+        if (gm == 2 && a.S % 8 != 0) gm = 1;
+        a.grid_map = (gm == 1 && gx % 8 == 0) ? 1 : (gm == 2) ? 2 : 0;
         const int nt = (int)g_opt[ECG_OPT_NT].load();
         Launcher l = nullptr;
         switch (mode) {

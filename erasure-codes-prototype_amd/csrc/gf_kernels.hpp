@@ -35,9 +35,9 @@ constexpr int kInlineSrc = 128;
 constexpr int kInlineDst = 32;
 constexpr int kMaxMT = 8;       // output rows per row tile
 #ifndef ECG_TPB
-#define ECG_TPB 256
+#define ECG_TPB 128
 #endif
-constexpr int kThreads = ECG_TPB;  // threads per workgroup (4 waves of 64); ECG_TPB only for tuning builds
+constexpr int kThreads = ECG_TPB;  // threads per workgroup (2 waves of 64, r01 tuning); ECG_TPB only for tuning builds
 
 struct GfLaunch {
     // programs: [nprog][rtiles][k][MT] tables, [nprog][k] src ids, [nprog][m] dst ids

@@ -45,8 +45,9 @@ void ecg_free(void* p);            /* frees matrices returned by this library (m
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
  * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP).  Results never depend on them. */
 #define ECG_OPT_NT 0           /* non-temporal policy: bit 0 = loads, bit 1 = stores (default 3) */
-#define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 256; 0 = auto (256) */
-#define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous (default), 2 = stripe s on XCD group s%8 */
+#define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 128; 0 = auto (128 = 2 KiB) */
+#define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous, 2 = stripe s on XCD group s%8,
+                                  3 = auto (default): 1 when outputs live inside the input stripes, else 2 */
 #define ECG_OPT_COUNT 3
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);

@@ -180,3 +180,20 @@ def test_bad_arguments(ecg):
     with pytest.raises(ecg.EcgError) as e:
         op.make_encoding_matrix()
     assert e.value.code == ecg.ECG_EUNPINNED
+
+
+def test_tuning_options_validation(ecg):
+    """ecg_set_option / ecg_get_option (include/ecg.h): range checks, defaults, no GPU needed."""
+    saved = [ecg.get_option(o) for o in range(3)]
+    try:
+        assert ecg.get_option(ecg.ECG_OPT_COUNT) == -1
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_NT, 4) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_COLS_PER_WG, 100) != 0  # not a multiple of the WG size
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_GRID_MAP, 4) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_COLS_PER_WG, 512) == 0
+        assert ecg.get_option(ecg.ECG_OPT_COLS_PER_WG) == 512
+    finally:
+        for o, v in enumerate(saved):
+            ecg.set_option(o, v)
+    if "ECG_GRID_MAP" not in os.environ:
+        assert saved[ecg.ECG_OPT_GRID_MAP] == 3  # auto

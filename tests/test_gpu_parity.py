@@ -483,3 +483,42 @@ def test_host_pipeline_encode_decode(ecg, oracle, torch_cuda, pinned):
     h[:, 5] = 0
     ecg.decode_batch_host(k, m, M, 1, [5], stripes, chunk_stripes=5)  # in place
     assert np.array_equal(h, orig)
+
+
+def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
+    """Every ECG_OPT_* setting (grid map incl. auto, NT policy, chunk size) gives identical bytes, for an
+    in-stripe encode, a separate-buffer decode and S values that do / do not divide by 8."""
+    torch = torch_cuda
+    k, m, B = 10, 4, 3 * 8192 + 16
+    n = k + m
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    saved = [ecg.get_option(o) for o in range(3)]
+    try:
+        for S in (16, 13):
+            stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+            ecg.fill_random(stripes, 21 + S)
+            ref_par, ref_dec = None, None
+            pos = (torch.arange(S, device="cuda", dtype=torch.int32) % n).contiguous()
+            for gmap, nt, cpw in itertools.product((0, 1, 2, 3), (0, 3), (0, 256)):
+                ecg.set_option(ecg.ECG_OPT_GRID_MAP, gmap)
+                ecg.set_option(ecg.ECG_OPT_NT, nt)
+                ecg.set_option(ecg.ECG_OPT_COLS_PER_WG, cpw)
+                stripes[:, k:].fill_(0xA5)
+                ecg.encode_batch(k, m, M, stripes[:, :k], stripes[:, k:])
+                out = torch.full((S, 1, B), 0x3C, dtype=torch.uint8, device="cuda")
+                ecg.decode_batch(k, m, M, 1, [[e] for e in range(n)], stripes, out=out, pattern_of_stripe=pos)
+                torch.cuda.synchronize()
+                if ref_par is None:
+                    ref_par, ref_dec = stripes[:, k:].clone(), out.clone()
+                    h = stripes.cpu().numpy()
+                    for s in (0, S - 1):
+                        par = [np.zeros(B, np.uint8) for _ in range(m)]
+                        oracle.jerasure_matrix_encode(k, m, M, [h[s, j] for j in range(k)], par, B)
+                        assert same([h[s, k + i] for i in range(m)], par)
+                    for s in range(S):
+                        assert torch.equal(out[s, 0], stripes[s, s % n])
+                assert torch.equal(stripes[:, k:], ref_par), (S, gmap, nt, cpw)
+                assert torch.equal(out, ref_dec), (S, gmap, nt, cpw)
+    finally:
+        for o, v in enumerate(saved):
+            ecg.set_option(o, v)

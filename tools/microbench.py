@@ -74,26 +74,39 @@ def main():
              2 * halfS * B),
             ("xor 10->1 defaults", opt(3, 0, 0, 1), lambda: ecg.perform_addition_batch(10, 1, data, rebuilt),
              S * 11 * B)]
-    for gmap in ((0, 1, 2) if not a.quick else ()):
-        variants.append((f"encode GENERAL cpw=256 map={gmap} nt=3", opt(3, 256, 0, gmap),
-                         lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes))
-        variants.append((f"decode rot14 cpw=256 map={gmap}", opt(3, 256, 0, gmap),
-                         lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=rebuilt, pattern_of_stripe=pos),
-                         dec_bytes))
-    for cpw in ((512, 768) if not a.quick else ()):
-        variants.append((f"encode GENERAL cpw={cpw} map=1 nt=3", opt(3, cpw, 0, 1),
-                         lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes))
+        for gmap in (1, 2):
+            variants += [
+                (f"encode map={gmap}", opt(3, 0, 0, gmap), lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes),
+                (f"decode rot14 map={gmap}", opt(3, 0, 0, gmap),
+                 lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=rebuilt, pattern_of_stripe=pos), dec_bytes),
+                (f"xor 10->1 map={gmap}", opt(3, 0, 0, gmap),
+                 lambda: ecg.perform_addition_batch(10, 1, data, rebuilt), S * 11 * B)]
     if not a.quick:
-        variants.append(("encode BINARY(ones) cpw=256 map=1", opt(3, 256, 0, 1),
+        for gmap in (0, 1, 2):
+            variants.append((f"encode GENERAL auto-cpw map={gmap}", opt(3, 0, 0, gmap),
+                             lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes))
+            variants.append((f"decode rot14 auto-cpw map={gmap}", opt(3, 0, 0, gmap),
+                             lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=rebuilt,
+                                                      pattern_of_stripe=pos), dec_bytes))
+        for cpw in (256, 512):
+            variants.append((f"encode GENERAL cpw={cpw} map=1", opt(3, cpw, 0, 1),
+                             lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes))
+            variants.append((f"decode rot14 cpw={cpw} map=1", opt(3, cpw, 0, 1),
+                             lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=rebuilt,
+                                                      pattern_of_stripe=pos), dec_bytes))
+        for nt in (0, 1, 2):
+            variants.append((f"encode GENERAL nt={nt}", opt(nt, 0, 0, 1),
+                             lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes))
+        variants.append(("encode BINARY(ones) defaults", opt(),
                          lambda: ecg.encode_batch(k, m, ones, data, coding), enc_bytes))
-    flat = stripes.view(S * n, 1, B)
-    halfS = S * n // 2
-    src1, dst1 = flat[:halfS], flat[halfS:2 * halfS]
-    for gmap in ((0, 1) if not a.quick else ()):
-        variants.append((f"copy 1->1 via engine map={gmap}", opt(3, 256, 0, gmap),
-                         lambda: ecg.perform_addition_batch(1, 1, src1, dst1), 2 * halfS * B))
-        variants.append((f"xor 10->1 map={gmap}", opt(3, 256, 0, gmap),
-                         lambda: ecg.perform_addition_batch(10, 1, data, rebuilt), S * 11 * B))
+        flat = stripes.view(S * n, 1, B)
+        halfS = S * n // 2
+        src1, dst1 = flat[:halfS], flat[halfS:2 * halfS]
+        for gmap in (0, 1):
+            variants.append((f"copy 1->1 via engine map={gmap}", opt(3, 0, 0, gmap),
+                             lambda: ecg.perform_addition_batch(1, 1, src1, dst1), 2 * halfS * B))
+            variants.append((f"xor 10->1 map={gmap}", opt(3, 0, 0, gmap),
+                             lambda: ecg.perform_addition_batch(10, 1, data, rebuilt), S * 11 * B))
     res = {name: [] for name, *_ in variants}
     for r in range(a.rounds):
         for name, setup, fn, nbytes in variants:
