@@ -432,8 +432,15 @@ def rs_host(a, r):
 def main():
     a = parse()
     r = D.from_env()
-    torch.cuda.set_device(r.local if r.distributed else 0)
-    D.init(r, "nccl", device=torch.device("cuda", r.local) if r.distributed else None)
+    # ECG_BENCH_SHARED_GPU=1: rehearsal of the N>1 path on a one-GPU box (every rank on cuda:0, gloo
+    # for the bookkeeping collectives).  Exercises the rank logic only; its timings mean nothing.
+    shared = os.environ.get("ECG_BENCH_SHARED_GPU") == "1"
+    dev = 0 if (shared or not r.distributed) else r.local
+    torch.cuda.set_device(dev)
+    if shared:
+        D.init(r, "gloo")
+    else:
+        D.init(r, "nccl", device=torch.device("cuda", dev) if r.distributed else None)
     ecg.lib().ecg_set_device(torch.cuda.current_device())
     fn = {"rs-encode-decode": rs_encode_decode, "lrc-repair": lrc_repair, "pc-merge": pc_merge,
           "rs4m-waves": rs4m_waves, "rs-host": rs_host}[a.workload]

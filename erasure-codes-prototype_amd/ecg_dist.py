@@ -33,7 +33,12 @@ def from_env() -> Rank:
                 int(os.environ.get("LOCAL_RANK", "0")))
 
 
+_BACKEND = None
+
+
 def init(r: Rank, backend: str = "nccl", device=None) -> None:
+    global _BACKEND
+    _BACKEND = backend
     if r.distributed and not dist.is_initialized():
         if device is not None:
             dist.init_process_group(backend, device_id=device)
@@ -59,9 +64,14 @@ def barrier(r: Rank) -> None:
         dist.barrier()
 
 
+def _dev(device):
+    return "cpu" if _BACKEND == "gloo" else device  # gloo collectives run on host tensors
+
+
 def _reduce(value: float, r: Rank, op, device) -> float:
     if not r.distributed:
         return value
+    device = _dev(device)
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=op)
     return float(t.item())
@@ -90,7 +100,7 @@ def gather_checksums(c: int, r: Rank, device="cpu") -> list[int]:
     if not r.distributed:
         return [c]
     v = c if c < (1 << 63) else c - (1 << 64)  # carry the 64-bit pattern in a signed tensor
-    t = torch.tensor([v], dtype=torch.int64, device=device)
+    t = torch.tensor([v], dtype=torch.int64, device=_dev(device))
     out = [torch.zeros_like(t) for _ in range(r.world)]
     dist.all_gather(out, t)
     return [int(x.item()) & _MASK64 for x in out]

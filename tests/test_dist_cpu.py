@@ -45,9 +45,11 @@ def _worker(rank, world, port, total, q):
     D.barrier(r)
     par = _encode_range(first, last, k, m, B, seed)
     c = D.checksum64(torch.from_numpy(par))
-    sums = D.gather_checksums(c, r)
-    t = D.max_over_ranks(float(rank + 1), r)
-    n = D.sum_over_ranks(float(last - first), r)
+    # device="cuda" as bench.py passes it: under gloo (bench's ECG_BENCH_SHARED_GPU rehearsal and these
+    # tests) ecg_dist keeps the bookkeeping tensors on the host
+    sums = D.gather_checksums(c, r, device="cuda")
+    t = D.max_over_ranks(float(rank + 1), r, device="cuda")
+    n = D.sum_over_ranks(float(last - first), r, device="cuda")
     D.barrier(r)
     q.put((rank, first, last, sums, t, n))
     torch.distributed.destroy_process_group()

@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Compare bench.py JSON lines of the N=1 and N=2 rehearsal runs (tools/gpu_dist_rehearsal.sh)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "erasure-codes-prototype_amd"))
+import ecg_dist as D  # noqa: E402
+
+
+def line(path):
+    for ln in reversed(open(path).read().splitlines()):
+        if ln.startswith("{"):
+            return json.loads(ln)
+    raise SystemExit(f"no JSON line in {path}")
+
+
+d = sys.argv[1]
+rs1, rs2 = line(f"{d}/rs_n1.log"), line(f"{d}/rs_n2.log")
+w1, w2 = line(f"{d}/waves_n1.log"), line(f"{d}/waves_n2.log")
+ok = True
+c1 = D.combine(int(x, 16) for x in rs1["parity_checksums"])
+c2 = D.combine(int(x, 16) for x in rs2["parity_checksums"])
+print(f"rs-encode-decode: N=1 512 stripes {c1:016x}; N=2 x 256 {c2:016x}; n_gpus={rs2['n_gpus']}")
+ok &= c1 == c2 and rs2["n_gpus"] == 2 and len(rs2["parity_checksums"]) == 2
+print(f"rs4m-waves: N=1 {w1['parity_checksum']}; N=2 {w2['parity_checksum']}")
+ok &= w1["parity_checksum"] == w2["parity_checksum"]
+for f in ("lrc_n2", "pc_n2"):
+    x = line(f"{d}/{f}.log")
+    print(f, "n_gpus", x["n_gpus"])
+    ok &= x["n_gpus"] == 2
+print("REHEARSAL", "OK" if ok else "MISMATCH")
+sys.exit(0 if ok else 1)
