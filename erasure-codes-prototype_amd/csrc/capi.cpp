@@ -25,6 +25,19 @@ int* to_malloc(const std::vector<int>& v) {
 
 std::vector<int> vec(const int* p, int n) { return n > 0 && p ? std::vector<int>(p, p + n) : std::vector<int>(); }
 
+void put_lists(std::vector<int>& out, const std::vector<std::vector<int>>& lists) {
+    out.push_back((int)lists.size());
+    for (auto& l : lists) {
+        out.push_back((int)l.size());
+        out.insert(out.end(), l.begin(), l.end());
+    }
+}
+
+int emit(const std::vector<int>& v, int* buf, int cap) {
+    if (buf && cap >= (int)v.size()) memcpy(buf, v.data(), v.size() * sizeof(int));
+    return (int)v.size();
+}
+
 }  // namespace
 
 extern "C" {
@@ -371,6 +384,67 @@ int ecg_ec_partial_encoding_matrix(ecg_ec* ec, const int* data_idxs, int n_data,
     if ((int)M.size() > out_cap) return ECG_EINVAL;
     memcpy(out_coef, M.data(), M.size() * sizeof(int));
     return n_parity;
+}
+
+// ---- partitioning and repair planning (planning.cpp)
+
+int ecg_ec_set_placement_rule(ecg_ec* ec, int rule) {
+    if (!ec || rule < ECG_PLACE_FLAT || rule > ECG_PLACE_SUB_OPTIMAL) return ECG_EINVAL;
+    ec->impl->placement_rule = rule;
+    return ECG_OK;
+}
+
+int ecg_ec_set_random_seed(ecg_ec* ec, unsigned long long seed) {
+    if (!ec) return ECG_EINVAL;
+    ec->impl->set_random_seed(seed);
+    return ECG_OK;
+}
+
+int ecg_ec_generate_partition(ecg_ec* ec) {
+    if (!ec) return ECG_EINVAL;
+    return ec->impl->generate_partition();
+}
+
+int ecg_ec_get_partition(ecg_ec* ec, int* buf, int cap) {
+    if (!ec || cap < 0) return ECG_EINVAL;
+    std::vector<int> out;
+    put_lists(out, ec->impl->partition_plan);
+    return emit(out, buf, cap);
+}
+
+int ecg_ec_grouping_information(ecg_ec* ec, int* buf, int cap) {
+    if (!ec || cap < 0) return ECG_EINVAL;
+    auto* lrc = dynamic_cast<LocallyRepairableCode*>(ec->impl);
+    if (!lrc) return ECG_EINVAL;
+    std::vector<std::vector<int>> groups;
+    lrc->grouping_information(groups);
+    std::vector<int> out;
+    put_lists(out, groups);
+    return emit(out, buf, cap);
+}
+
+int ecg_ec_generate_repair_plan(ecg_ec* ec, const int* failure_idxs, int n, int* buf, int cap, int* decodable) {
+    if (!ec || n <= 0 || !failure_idxs || cap < 0) return ECG_EINVAL;
+    std::vector<RepairPlan> plans;
+    const int rc = ec->impl->generate_repair_plan(vec(failure_idxs, n), plans);
+    if (rc < 0) return rc;
+    if (decodable) *decodable = rc;
+    std::vector<int> out;
+    out.push_back((int)plans.size());
+    for (auto& p : plans) {
+        out.push_back(p.local_or_column ? 1 : 0);
+        out.push_back((int)p.failure_idxs.size());
+        out.insert(out.end(), p.failure_idxs.begin(), p.failure_idxs.end());
+        put_lists(out, p.help_blocks);
+    }
+    return emit(out, buf, cap);
+}
+
+int ecg_ec_self_information(ecg_ec* ec, char* buf, int cap) {
+    if (!ec || cap < 0) return ECG_EINVAL;
+    const std::string s = ec->impl->self_information();
+    if (buf && cap > (int)s.size()) memcpy(buf, s.c_str(), s.size() + 1);
+    return (int)s.size();
 }
 
 }  // extern "C"

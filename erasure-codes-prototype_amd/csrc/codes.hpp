@@ -8,10 +8,12 @@
 //   * methods return int status instead of void (the reference prints and returns);
 //   * blocks may be host (reference semantics) or device pointers (`mem`, `stream`);
 //   * coding matrices are cached per object instead of rebuilt per call (rs.cpp:22-23).
-// Out of scope: repair planning, partitioning and placement logic.
+// Partitioning (placement of a stripe's blocks over clusters) and repair planning (which helper blocks each
+// cluster contributes to a partial-decoding repair) are host logic in planning.cpp.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <memory>
 #include <string>
 #include <vector>
@@ -22,6 +24,13 @@
 namespace ecg {
 
 using CodingParameters = ecg_coding_parameters;
+
+// erasure_code.h:53-58.  help_blocks[i] = the blocks one cluster (partition) contributes.
+struct RepairPlan {
+    bool local_or_column = false;
+    std::vector<int> failure_idxs;
+    std::vector<std::vector<int>> help_blocks;
+};
 
 // A call's work: ops over block ids, ids index `blocks` (data_ptrs then coding_ptrs).
 struct Plan {
@@ -69,6 +78,21 @@ public:
 
     virtual std::string self_information() const = 0;
 
+    // ---- partitioning and repair planning (planning.cpp)
+    int placement_rule = ECG_PLACE_OPTIMAL;  // erasure_code.h:66 default OPTIMAL
+    std::vector<std::vector<int>> partition_plan;
+    virtual void partition_flat();
+    virtual void partition_random() = 0;
+    virtual void partition_optimal() = 0;
+    virtual int partition_sub_optimal() { return ECG_EINVAL; }  // Azu_LRC only
+    int generate_partition();  // erasure_code.cpp:159-169 (+ ECG_PLACE_SUB_OPTIMAL)
+    // 1 = plans generated, 0 = undecodable (the reference's bool), < 0 = bad arguments
+    virtual int generate_repair_plan(const std::vector<int>& failure_idxs, std::vector<RepairPlan>& plans) = 0;
+    void set_random_seed(uint64_t seed) {
+        rng_ = seed;
+        rng_seeded_ = true;
+    }
+
     // erasure_code.cpp:30-61
     static void get_full_matrix(int* matrix, int kk);
     static void make_submatrix_by_rows(int cols, const int* matrix, int* new_matrix, const std::vector<int>& idxs);
@@ -82,6 +106,15 @@ public:
                                          const std::vector<int>& failure_idxs, std::vector<int>& out);
 
 protected:
+    // random_range / random_index (utils.cpp:6-21): the reference draws from a fresh random_device-seeded
+    // mt19937 per call; here a per-object splitmix64 stream (seeded from random_device, or explicitly for
+    // reproducible placements).  Same support, uniform.
+    uint64_t rng_ = 0;
+    bool rng_seeded_ = false;
+    uint64_t next_random();
+    int random_range(int lo, int hi);
+    int random_index(int len);
+
     // Execute a plan over data_ptrs (n_data) ++ coding_ptrs (n_coding) on this object's memory tier.
     int run(const Plan& plan, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding, long long B);
     // jerasure_matrix_encode / _decode over this call's pointers
@@ -104,6 +137,13 @@ public:
     int partial_decoding_matrix(std::vector<int> lsi, std::vector<int> si, std::vector<int> fi,
                                 std::vector<int>& out) override;
     std::string self_information() const override;
+
+    void partition_random() override;   // rs.cpp:78-101
+    void partition_optimal() override;  // rs.cpp:103-116
+    void help_blocks_for_single_block_repair_oneoff(int failure_idx, std::vector<std::vector<int>>& help_blocks);
+    void help_blocks_for_multi_blocks_repair_oneoff(const std::vector<int>& failure_idxs,
+                                                    std::vector<std::vector<int>>& help_blocks);
+    int generate_repair_plan(const std::vector<int>& failure_idxs, std::vector<RepairPlan>& plans) override;
 
     // Plans over an arbitrary id space (used by the product codes)
     int plan_encode(Plan& p, const std::vector<int>& data_ids, const std::vector<int>& coding_ids);
@@ -154,6 +194,15 @@ public:
     virtual int bid2gid(int block_id) = 0;
     virtual int idxingroup(int block_id) = 0;
 
+    virtual void grouping_information(std::vector<std::vector<int>>& groups) = 0;
+    void partition_random() override;   // lrc.cpp:215-238
+    void partition_optimal() override {}  // lrc.h:75
+    virtual void help_blocks_for_single_block_repair_oneoff(int failure_idx,
+                                                            std::vector<std::vector<int>>& help_blocks);
+    void help_blocks_for_multi_blocks_repair_oneoff(const std::vector<int>& failure_idxs,
+                                                    std::vector<std::vector<int>>& help_blocks);
+    int generate_repair_plan(const std::vector<int>& failure_idxs, std::vector<RepairPlan>& plans) override;
+
 protected:
     std::vector<int> full_matrix();                        // [I_k ; G ; L]
     std::vector<int> group_full_matrix(int group_size, int group_id);  // [I_gs ; group row]
@@ -171,6 +220,9 @@ public:
     int idxingroup(int block_id) override;
     int check_if_decodable(const std::vector<int>& failure_idxs) override;
     std::string self_information() const override;
+    void grouping_information(std::vector<std::vector<int>>& groups) override;  // lrc.cpp:706-723
+    void partition_optimal() override;                                            // lrc.cpp:725-814
+    int partition_sub_optimal() override;                                         // lrc.cpp:816-873
 };
 
 class Azu_LRC_1 : public LocallyRepairableCode {
@@ -182,6 +234,9 @@ public:
     int bid2gid(int block_id) override;
     int idxingroup(int block_id) override;
     std::string self_information() const override;
+    int check_if_decodable(const std::vector<int>& failure_idxs) override;      // lrc.cpp:881-931
+    void grouping_information(std::vector<std::vector<int>>& groups) override;  // lrc.cpp:1051-1069
+    void partition_optimal() override;                                            // lrc.cpp:1071-1088
 };
 
 class Opt_LRC : public LocallyRepairableCode {
@@ -193,6 +248,9 @@ public:
     int bid2gid(int block_id) override;
     int idxingroup(int block_id) override;
     std::string self_information() const override;
+    int check_if_decodable(const std::vector<int>& failure_idxs) override;      // lrc.cpp:1096-1166
+    void grouping_information(std::vector<std::vector<int>>& groups) override;  // lrc.cpp:1270-1282
+    void partition_optimal() override;                                            // lrc.cpp:1284-1301
 };
 
 class Opt_Cau_LRC : public LocallyRepairableCode {
@@ -204,6 +262,13 @@ public:
     int bid2gid(int block_id) override;
     int idxingroup(int block_id) override;
     std::string self_information() const override;
+    int check_if_decodable(const std::vector<int>& failure_idxs) override;      // lrc.cpp:1415-1483
+    void grouping_information(std::vector<std::vector<int>>& groups) override;  // lrc.cpp:1641-1658
+    void partition_optimal() override;                                            // lrc.cpp:1660-1749
+    void help_blocks_for_single_block_repair_oneoff(int failure_idx,
+                                                    std::vector<std::vector<int>>& help_blocks) override;
+    int generate_repair_plan(const std::vector<int>& failure_idxs, std::vector<RepairPlan>& plans) override;
+    int surviving_group_id = 0;  // lrc.h:171 (uninitialised in the reference; only read after being set)
 
 protected:
     int remap_local(int idx, int group_size, int min_idx) const override;
@@ -219,6 +284,9 @@ public:
     int bid2gid(int block_id) override;
     int idxingroup(int block_id) override;
     std::string self_information() const override;
+    int check_if_decodable(const std::vector<int>& failure_idxs) override;      // lrc.cpp:2025-2095
+    void grouping_information(std::vector<std::vector<int>>& groups) override;  // lrc.cpp:2273-2285
+    void partition_optimal() override;                                            // lrc.cpp:2287-2304
 
 protected:
     bool cauchy_based() const override { return true; }
@@ -248,6 +316,11 @@ public:
     int rowcol2bid(int row, int col) const;
     void bid2rowcol(int bid, int& row, int& col) const;
     virtual int oldbid2newbid_for_merge(int old_block_id, int x, int seri_num, bool isvertical);
+
+    void partition_flat() override;     // pc.cpp:378-388
+    void partition_random() override;   // pc.cpp:390-421
+    void partition_optimal() override;  // pc.cpp:423-443
+    int generate_repair_plan(const std::vector<int>& failure_idxs, std::vector<RepairPlan>& plans) override;
 
 protected:
     virtual RSCode& rowc() { return row_code; }  // code used for rows in encode/decode
@@ -283,6 +356,8 @@ public:
     int decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) override;
     int check_if_decodable(const std::vector<int>& failure_idxs) override;
     std::string self_information() const override;
+    void partition_random() override;   // pc.cpp:1091-1129
+    void partition_optimal() override;  // pc.cpp:1131-1158
 
 protected:
     bool has_global() const override { return false; }

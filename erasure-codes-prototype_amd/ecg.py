@@ -39,6 +39,20 @@ ECG_OPT_COUNT = 3
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 
+
+class PlacementRule(IntEnum):  # include/ec/erasure_code.h:31-36 (+ Azure sub-optimal)
+    FLAT = 0
+    RANDOM = 1
+    OPTIMAL = 2
+    SUB_OPTIMAL = 3
+
+
+@dataclass
+class RepairPlan:  # include/ec/erasure_code.h:53-58
+    local_or_column: bool
+    failure_idxs: list
+    help_blocks: list
+
 # Every symbol include/ecg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free",
@@ -56,6 +70,8 @@ EXPORTS = [
     "ecg_ec_check_if_decodable", "ecg_ec_encode", "ecg_ec_decode",
     "ecg_ec_encode_partial_blocks_for_encoding", "ecg_ec_encode_partial_blocks_for_decoding",
     "ecg_ec_perform_addition", "ecg_ec_partial_decoding_matrix", "ecg_ec_partial_encoding_matrix",
+    "ecg_ec_set_placement_rule", "ecg_ec_set_random_seed", "ecg_ec_generate_partition", "ecg_ec_get_partition",
+    "ecg_ec_grouping_information", "ecg_ec_generate_repair_plan", "ecg_ec_self_information",
 ]
 
 
@@ -164,6 +180,13 @@ def lib():
         "ecg_ec_perform_addition": ([P, PP, PP, I, I, I], I),
         "ecg_ec_partial_decoding_matrix": ([P, IP, I, IP, I, IP, I, IP, I], I),
         "ecg_ec_partial_encoding_matrix": ([P, IP, I, IP, I, IP, I], I),
+        "ecg_ec_set_placement_rule": ([P, I], I),
+        "ecg_ec_set_random_seed": ([P, ULL], I),
+        "ecg_ec_generate_partition": ([P], I),
+        "ecg_ec_get_partition": ([P, IP, I], I),
+        "ecg_ec_grouping_information": ([P, IP, I], I),
+        "ecg_ec_generate_repair_plan": ([P, IP, I, IP, I, IP], I),
+        "ecg_ec_self_information": ([P, ctypes.c_char_p, I], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -486,6 +509,72 @@ class ErasureCode:
         _check(lib().ecg_ec_partial_encoding_matrix(self._h, _ints(data_idxs), len(data_idxs), _ints(parity_idxs),
                                                     len(parity_idxs), out, cap), "partial_encoding_matrix")
         return list(out)[:len(data_idxs) * len(parity_idxs)]
+
+
+    # --- partitioning and repair planning (csrc/planning.cpp)
+    @property
+    def placement_rule(self):
+        return self._rule if hasattr(self, "_rule") else PlacementRule.OPTIMAL
+
+    @placement_rule.setter
+    def placement_rule(self, rule):
+        _check(lib().ecg_ec_set_placement_rule(self._h, int(rule)), "placement_rule")
+        self._rule = PlacementRule(int(rule))
+
+    def set_random_seed(self, seed):
+        _check(lib().ecg_ec_set_random_seed(self._h, seed & ((1 << 64) - 1)), "set_random_seed")
+
+    def generate_partition(self):  # erasure_code.cpp:159-169
+        _check(lib().ecg_ec_generate_partition(self._h), "generate_partition")
+        return self.partition_plan
+
+    @staticmethod
+    def _call_sized(fn, what):
+        n = _check(fn(None, 0), what)
+        buf = (ctypes.c_int * max(1, n))()
+        _check(fn(buf, n), what)
+        return list(buf)[:n]
+
+    @staticmethod
+    def _lists(v, at):
+        n = v[at]
+        at += 1
+        out = []
+        for _ in range(n):
+            sz = v[at]
+            out.append(v[at + 1:at + 1 + sz])
+            at += 1 + sz
+        return out, at
+
+    @property
+    def partition_plan(self):
+        v = self._call_sized(lambda b, c: lib().ecg_ec_get_partition(self._h, b, c), "get_partition")
+        return self._lists(v, 0)[0]
+
+    def grouping_information(self):  # LRC only (lrc.h:73)
+        v = self._call_sized(lambda b, c: lib().ecg_ec_grouping_information(self._h, b, c), "grouping_information")
+        return self._lists(v, 0)[0]
+
+    def generate_repair_plan(self, failure_idxs):
+        """Returns (decodable, [RepairPlan]) like the reference's bool + out-parameter."""
+        dec = ctypes.c_int(0)
+        fi = _ints(failure_idxs)
+        v = self._call_sized(lambda b, c: lib().ecg_ec_generate_repair_plan(self._h, fi, len(failure_idxs), b, c,
+                                                                            ctypes.byref(dec)),
+                             "generate_repair_plan")
+        plans, at = [], 1
+        for _ in range(v[0]):
+            loc, nf = bool(v[at]), v[at + 1]
+            fails = v[at + 2:at + 2 + nf]
+            helps, at = self._lists(v, at + 2 + nf)
+            plans.append(RepairPlan(loc, fails, helps))
+        return bool(dec.value), plans
+
+    def self_information(self):
+        n = _check(lib().ecg_ec_self_information(self._h, None, 0), "self_information")
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().ecg_ec_self_information(self._h, buf, n + 1)
+        return buf.value.decode()
 
 
 def ec_factory(ec_type, cp: CodingParameters) -> ErasureCode:  # project/src/metadata.cpp:48-77

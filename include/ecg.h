@@ -179,6 +179,31 @@ int ecg_ec_partial_decoding_matrix(ecg_ec* ec, const int* local_survivor_idxs, i
 int ecg_ec_partial_encoding_matrix(ecg_ec* ec, const int* data_idxs, int n_data, const int* parity_idxs,
                                    int n_parity, int* out_coef, int out_cap);
 
+/* ---- partitioning and repair planning (host logic) ----
+ * Placement rules: erasure_code.h:31-36 PlacementRule, plus Azu_LRC::partition_sub_optimal
+ * (lrc.cpp:816-873), which the reference defines but never reaches from generate_partition. */
+#define ECG_PLACE_FLAT 0
+#define ECG_PLACE_RANDOM 1
+#define ECG_PLACE_OPTIMAL 2     /* the reference's default (erasure_code.h:66) */
+#define ECG_PLACE_SUB_OPTIMAL 3 /* Azure LRC only */
+int ecg_ec_set_placement_rule(ecg_ec* ec, int rule);
+/* Seed of the per-object stream behind RANDOM placement (default: std::random_device). */
+int ecg_ec_set_random_seed(ecg_ec* ec, unsigned long long seed);
+/* ErasureCode::generate_partition (erasure_code.cpp:159-169). */
+int ecg_ec_generate_partition(ecg_ec* ec);
+/* The current partition_plan, serialised as [n_partitions, (size, block ids...)*].  Returns the number
+ * of ints the encoding needs; `buf` is written only when cap >= that number. */
+int ecg_ec_get_partition(ecg_ec* ec, int* buf, int cap);
+/* LRC grouping_information (lrc.h:73): [n_groups, (size, block ids...)*]; ECG_EINVAL for other codes. */
+int ecg_ec_grouping_information(ecg_ec* ec, int* buf, int cap);
+/* ErasureCode::generate_repair_plan (rs.cpp:264-279, lrc.cpp:445-574 / 1861-2023, pc.cpp:451-551 /
+ * 1166-1264) over the current partition_plan.  *decodable = 1 (plans made) or 0 (undecodable; the
+ * reference's false).  Plans serialised as [n_plans, (local_or_column, n_failures, ids...,
+ * n_help, (size, ids...)*)*].  Returns the number of ints needed (written when cap suffices) or < 0. */
+int ecg_ec_generate_repair_plan(ecg_ec* ec, const int* failure_idxs, int n, int* buf, int cap, int* decodable);
+/* ErasureCode::self_information (e.g. "RS(10,4)"); returns the length, writes when cap > length. */
+int ecg_ec_self_information(ecg_ec* ec, char* buf, int cap);
+
 #ifdef __cplusplus
 }
 #endif
