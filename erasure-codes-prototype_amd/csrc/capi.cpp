@@ -412,6 +412,25 @@ int ecg_ec_get_partition(ecg_ec* ec, int* buf, int cap) {
     return emit(out, buf, cap);
 }
 
+int ecg_ec_set_partition(ecg_ec* ec, const int* buf, int len) {
+    if (!ec || !buf || len < 1) return ECG_EINVAL;
+    const int n_blocks = ec->impl->k + ec->impl->m;
+    std::vector<std::vector<int>> plan;
+    int at = 1;
+    for (int p = 0; p < buf[0]; p++) {
+        if (at >= len) return ECG_EINVAL;
+        const int sz = buf[at++];
+        if (sz < 0 || at + sz > len) return ECG_EINVAL;
+        std::vector<int> part(buf + at, buf + at + sz);
+        for (int b : part)
+            if (b < 0 || b >= n_blocks) return ECG_EINVAL;
+        plan.push_back(part);
+        at += sz;
+    }
+    ec->impl->partition_plan = plan;
+    return ECG_OK;
+}
+
 int ecg_ec_grouping_information(ecg_ec* ec, int* buf, int cap) {
     if (!ec || cap < 0) return ECG_EINVAL;
     auto* lrc = dynamic_cast<LocallyRepairableCode*>(ec->impl);
@@ -438,6 +457,40 @@ int ecg_ec_generate_repair_plan(ecg_ec* ec, const int* failure_idxs, int n, int*
         put_lists(out, p.help_blocks);
     }
     return emit(out, buf, cap);
+}
+
+int ecg_ec_bid2gid(ecg_ec* ec, int block_id) {
+    auto* lrc = ec ? dynamic_cast<LocallyRepairableCode*>(ec->impl) : nullptr;
+    if (!lrc || block_id < 0 || block_id >= lrc->k + lrc->m) return ECG_EINVAL;
+    return lrc->bid2gid(block_id);
+}
+
+int ecg_ec_idxingroup(ecg_ec* ec, int block_id) {
+    auto* lrc = ec ? dynamic_cast<LocallyRepairableCode*>(ec->impl) : nullptr;
+    if (!lrc || block_id < 0 || block_id >= lrc->k + lrc->m) return ECG_EINVAL;
+    return lrc->idxingroup(block_id);
+}
+
+int ecg_ec_get_group_size(ecg_ec* ec, int group_id, int* min_idx) {
+    auto* lrc = ec ? dynamic_cast<LocallyRepairableCode*>(ec->impl) : nullptr;
+    if (!lrc || group_id < 0 || group_id > lrc->l) return ECG_EINVAL;
+    int mi = 0;
+    const int gs = lrc->get_group_size(group_id, mi);
+    if (min_idx) *min_idx = mi;
+    return gs;
+}
+
+int ecg_ec_bid2rowcol(ecg_ec* ec, int block_id, int* row, int* col) {
+    auto* pc = ec ? dynamic_cast<ProductCode*>(ec->impl) : nullptr;
+    if (!pc || !row || !col || block_id < 0 || block_id >= pc->k + pc->m) return ECG_EINVAL;
+    pc->bid2rowcol(block_id, *row, *col);
+    return ECG_OK;
+}
+
+int ecg_ec_rowcol2bid(ecg_ec* ec, int row, int col) {
+    auto* pc = ec ? dynamic_cast<ProductCode*>(ec->impl) : nullptr;
+    if (!pc || row < 0 || col < 0 || row >= pc->k2 + pc->m2 || col >= pc->k1 + pc->m1) return ECG_EINVAL;
+    return pc->rowcol2bid(row, col);
 }
 
 int ecg_ec_self_information(ecg_ec* ec, char* buf, int cap) {

@@ -71,7 +71,8 @@ EXPORTS = [
     "ecg_ec_encode_partial_blocks_for_encoding", "ecg_ec_encode_partial_blocks_for_decoding",
     "ecg_ec_perform_addition", "ecg_ec_partial_decoding_matrix", "ecg_ec_partial_encoding_matrix",
     "ecg_ec_set_placement_rule", "ecg_ec_set_random_seed", "ecg_ec_generate_partition", "ecg_ec_get_partition",
-    "ecg_ec_grouping_information", "ecg_ec_generate_repair_plan", "ecg_ec_self_information",
+    "ecg_ec_set_partition", "ecg_ec_grouping_information", "ecg_ec_generate_repair_plan", "ecg_ec_self_information",
+    "ecg_ec_bid2gid", "ecg_ec_idxingroup", "ecg_ec_get_group_size", "ecg_ec_bid2rowcol", "ecg_ec_rowcol2bid",
 ]
 
 
@@ -184,9 +185,15 @@ def lib():
         "ecg_ec_set_random_seed": ([P, ULL], I),
         "ecg_ec_generate_partition": ([P], I),
         "ecg_ec_get_partition": ([P, IP, I], I),
+        "ecg_ec_set_partition": ([P, IP, I], I),
         "ecg_ec_grouping_information": ([P, IP, I], I),
         "ecg_ec_generate_repair_plan": ([P, IP, I, IP, I, IP], I),
         "ecg_ec_self_information": ([P, ctypes.c_char_p, I], I),
+        "ecg_ec_bid2gid": ([P, I], I),
+        "ecg_ec_idxingroup": ([P, I], I),
+        "ecg_ec_get_group_size": ([P, I, IP], I),
+        "ecg_ec_bid2rowcol": ([P, I, IP, IP], I),
+        "ecg_ec_rowcol2bid": ([P, I, I], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -550,6 +557,13 @@ class ErasureCode:
     def partition_plan(self):
         v = self._call_sized(lambda b, c: lib().ecg_ec_get_partition(self._h, b, c), "get_partition")
         return self._lists(v, 0)[0]
+
+    @partition_plan.setter
+    def partition_plan(self, plan):
+        flat = [len(plan)]
+        for part in plan:
+            flat += [len(part)] + list(part)
+        _check(lib().ecg_ec_set_partition(self._h, _ints(flat), len(flat)), "set_partition")
 
     def grouping_information(self):  # LRC only (lrc.h:73)
         v = self._call_sized(lambda b, c: lib().ecg_ec_grouping_information(self._h, b, c), "grouping_information")

@@ -194,6 +194,9 @@ int ecg_ec_generate_partition(ecg_ec* ec);
 /* The current partition_plan, serialised as [n_partitions, (size, block ids...)*].  Returns the number
  * of ints the encoding needs; `buf` is written only when cap >= that number. */
 int ecg_ec_get_partition(ecg_ec* ec, int* buf, int cap);
+/* Overwrite partition_plan (same encoding as ecg_ec_get_partition), as the coordinator does from the
+ * actual block placement before planning a repair (auxs.cpp:139-159). */
+int ecg_ec_set_partition(ecg_ec* ec, const int* buf, int len);
 /* LRC grouping_information (lrc.h:73): [n_groups, (size, block ids...)*]; ECG_EINVAL for other codes. */
 int ecg_ec_grouping_information(ecg_ec* ec, int* buf, int cap);
 /* ErasureCode::generate_repair_plan (rs.cpp:264-279, lrc.cpp:445-574 / 1861-2023, pc.cpp:451-551 /
@@ -201,6 +204,14 @@ int ecg_ec_grouping_information(ecg_ec* ec, int* buf, int cap);
  * reference's false).  Plans serialised as [n_plans, (local_or_column, n_failures, ids...,
  * n_help, (size, ids...)*)*].  Returns the number of ints needed (written when cap suffices) or < 0. */
 int ecg_ec_generate_repair_plan(ecg_ec* ec, const int* failure_idxs, int n, int* buf, int cap, int* decodable);
+/* Block-index helpers the coordinator and proxies use.  LRC (lrc.h:67-71): group of a block, its index in
+ * the group's encoding space, group size (+ first block id).  Product codes (pc.h:44-45): grid position.
+ * ECG_EINVAL when the code has no such notion. */
+int ecg_ec_bid2gid(ecg_ec* ec, int block_id);
+int ecg_ec_idxingroup(ecg_ec* ec, int block_id);
+int ecg_ec_get_group_size(ecg_ec* ec, int group_id, int* min_idx);
+int ecg_ec_bid2rowcol(ecg_ec* ec, int block_id, int* row, int* col);
+int ecg_ec_rowcol2bid(ecg_ec* ec, int row, int col);
 /* ErasureCode::self_information (e.g. "RS(10,4)"); returns the length, writes when cap > length. */
 int ecg_ec_self_information(ecg_ec* ec, char* buf, int cap);
 

@@ -257,6 +257,33 @@ def test_lrc_local_decode_side_channel(ecg, oracle, torch_cuda):
         assert np.array_equal(A[lost], group[lost])
 
 
+@pytest.mark.parametrize("t", [5, 6])  # OPTIMAL_CAUCHY_LRC, UNIFORM_CAUCHY_LRC
+def test_cauchy_local_decode_quirk(ecg, oracle, torch_cuda, t):
+    """decode_local hands failed_num to jerasure_matrix_decode as row_k_ones (lrc.cpp:58-71).  The Cauchy
+    LRCs' group rows are not all ones, so Jerasure's "last drive" XOR shortcut rebuilds a lost data block
+    wrongly — the engine must reproduce the reference's (wrong) bytes exactly, not silently fix them."""
+    from oracle import ec_ref as E
+    B = 1024
+    o, p = _pair(t, dict(k=8, l=2, g=2), local=True)
+    gs, _ = o.get_group_size(0)
+    row = o.make_group_matrix(0, gs)
+    assert any(c != 1 for c in row)  # the premise of the quirk
+    group = E.blocks(gs, B, 3)
+    local = E.zeros(1, B)
+    oracle.jerasure_matrix_encode(gs, 1, row, group, local, B)
+    wrong = 0
+    for lost in range(gs):
+        A = [x.copy() for x in group] + [local[0].copy()]
+        Bq = [x.copy() for x in A]
+        A[lost][:] = 0
+        Bq[lost][:] = 0
+        o.decode(A[:gs], A[gs:], B, [lost, 0], 1)
+        assert p.decode(Bq[:gs], Bq[gs:], B, [lost, 0], 1) == 0
+        assert np.array_equal(A[lost], Bq[lost]), lost  # bit-exact with the reference restatement
+        wrong += not np.array_equal(Bq[lost], group[lost])
+    assert wrong > 0  # and the quirk is real: some lost blocks come back wrong, as in the reference
+
+
 # ------------------------------------------------------------------ device tier + batches
 
 def test_device_tier_aligned_and_unaligned(ecg, oracle, torch_cuda):
