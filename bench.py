@@ -303,7 +303,7 @@ def pc_merge(a, r):
     """PC(4,1,4,1), 4 MiB blocks, merge x=2 HORIZONTAL: merged PC(8,1,4,1) row r parity = XOR of the
     two old stripes' row-r data blocks (r < 4) / column-parity blocks (r = 4); the RS(8,1) row code is all
     ones (main_recal / help_recal, handle_merge.cpp:159,269,319,453).  One launch reads 40 blocks and
-    writes 5 per merge (the algorithmic minimum, 9 * B per row)."""
+    writes 5 per merge (the algorithmic minimum, 9 * B per row).  Two formulations are timed (below)."""
     B = a.block_size or (4 << 20)
     S = a.stripes or 512
     old = ecg.ec_factory(ecg.ECTYPE.PC, ecg.CodingParameters(k1=4, m1=1, k2=4, m2=1))
@@ -321,34 +321,46 @@ def pc_merge(a, r):
     for row in range(5):
         coef.append([1 if j // 8 == row else 0 for j in range(40)])
     out = torch.empty((S, 5, B), dtype=torch.uint8, device="cuda")
-    prog = [(coef, src, [0, 1, 2, 3, 4])]
-
-    def step(ev=None):
-        if ev:
-            ev[0].record()
-        ecg.matrix_apply_batch_multi(prog, blocks, out)
-        if ev:
-            ev[1].record()
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    # check merges 0 and S-1 against XOR on the host
-    for s in (0, S - 1):
-        hb = blocks[s].cpu().numpy()
-        for row in range(5):
-            x = 0
-            for half in range(2):
-                for col in range(4):
-                    x = hb[half * nb + bid(row, col)] ^ x
-            assert (out[s, row].cpu().numpy() == x).all(), "merge mismatch"
-    elapsed, evs = timed_loop(r, a.steps, step)
-    t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+    # "fused": one 40 -> 5 BINARY program per merge (every workgroup streams all 40 blocks).
+    # "rows": the row parities are independent 8 -> 1 XORs, so each (merge, row) is its own launch stripe:
+    #   program r reads its row's 8 blocks, launch stripe i = (merge i // 5, row i % 5).
+    fused = [(coef, src, [0, 1, 2, 3, 4])]
+    rows = [([[1] * 8], src[8 * row:8 * row + 8], [row]) for row in range(5)]
+    prog_of = (torch.arange(5 * S, device="cuda", dtype=torch.int32) % 5).contiguous()
+    stripe_of = (torch.arange(5 * S, device="cuda", dtype=torch.int32) // 5).contiguous()
+    variants = {
+        "rows": lambda: ecg.matrix_apply_batch_multi(rows, blocks, out, prog_of_stripe=prog_of, stripe_of=stripe_of),
+        "fused": lambda: ecg.matrix_apply_batch_multi(fused, blocks, out),
+    }
     alg = S * 45 * B
+    res = {}
+    for name, fn in variants.items():
+        def step(ev=None, fn=fn):
+            if ev:
+                ev[0].record()
+            fn()
+            if ev:
+                ev[1].record()
+
+        out.zero_()
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        for s in (0, S // 2 + 1, S - 1):  # merges checked against XOR on the host
+            hb = blocks[s].cpu().numpy()
+            for row in range(5):
+                x = 0
+                for half in range(2):
+                    for col in range(4):
+                        x = hb[half * nb + bid(row, col)] ^ x
+                assert (out[s, row].cpu().numpy() == x).all(), f"merge mismatch ({name})"
+        elapsed, evs = timed_loop(r, a.steps, step)
+        t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+        res[name] = {"ms_per_batch": round(t * 1e3, 3), "merges_per_s": round(r.world * S * a.steps / elapsed, 1),
+                     "algorithmic_GBps": round(alg / t / 1e9, 1),
+                     "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
     return {"workload": "PC(4,1,4,1) merge x=2 horizontal, 4 MiB blocks", "n_gpus": r.world,
-            "merges_per_gpu": S, "steps": a.steps, "ms_per_batch": round(t * 1e3, 3),
-            "merges_per_s": round(r.world * S * a.steps / elapsed, 1),
-            "algorithmic_GBps": round(alg / t / 1e9, 1), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+            "merges_per_gpu": S, "steps": a.steps, "results": res,
             "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
