@@ -559,6 +559,50 @@ struct Loopback::Impl {
         return ok(ecg_ec_encode_partial_blocks_for_encoding(ec.h, dp.data(), op.data(), (int)B, orig_idx.data(),
                                                             (int)orig_idx.size(), p.parity_idx.data(), np));
     }
+
+    // main_recal + help_recal of one parity-recalculation plan: helpers on their own threads, the main
+    // proxy here (merge.cpp:405-425 / 1395-1415).
+    bool run_recal(const RecalCall& main, const std::vector<RecalCall>& helps, std::vector<Block>& parities) {
+        Channel chan;
+        std::vector<std::thread> threads;
+        std::vector<char> help_ok(helps.size(), 1);
+        for (size_t i = 0; i < helps.size(); i++)
+            threads.emplace_back([&, i] { help_ok[i] = help_recal(helps[i], chan); });
+        bool good = main_recal(main, chan, parities);
+        for (auto& t : threads) t.join();
+        return good && std::find(help_ok.begin(), help_ok.end(), 0) == help_ok.end();
+    }
+
+    // group the (new index, block id, node) inputs of one recalculation by cluster, in order of first
+    // appearance; the parity cluster's blocks are the main proxy's own, the others become helpers
+    void split_recal(RecalCall& main, const std::vector<BlockLoc>& inputs, std::vector<RecalCall>& helps) {
+        std::vector<std::pair<int, std::vector<BlockLoc>>> clusters;
+        for (auto& b : inputs) {
+            const int c = topo.cluster_of(b.node);
+            auto it = std::find_if(clusters.begin(), clusters.end(), [&](auto& e) { return e.first == c; });
+            if (it == clusters.end()) {
+                clusters.push_back({c, {}});
+                it = clusters.end() - 1;
+            }
+            it->second.push_back(b);
+        }
+        for (auto& c : clusters) {
+            if (c.first == main.cluster_id) {
+                main.inner.insert(main.inner.end(), c.second.begin(), c.second.end());
+            } else {
+                RecalCall h;
+                h.ec_type = main.ec_type;
+                h.cp = main.cp;
+                h.cluster_id = c.first;
+                h.block_size = main.block_size;
+                h.partial_decoding = main.partial_decoding;
+                h.parity_idx = main.parity_idx;
+                h.inner = c.second;
+                main.help.push_back(c.second);
+                helps.push_back(h);
+            }
+        }
+    }
 };
 
 // ================================================================ Loopback
@@ -635,7 +679,9 @@ bool Loopback::set(const std::string& key, const std::vector<char>& value) {
         if (!I.store.store_data(I.topo.node_port(s.blocks2nodes[j]), key_of(s.block_ids[j]), src, B)) return false;
     }
     s.objects.push_back(key);
-    objects_[key] = {s.stripe_id, 0};
+    std::vector<int> data_blocks(s.k);
+    for (int j = 0; j < s.k; j++) data_blocks[j] = j;
+    objects_[key] = {s.stripe_id, data_blocks};
     if (I.merge_groups.empty() || (int)I.merge_groups.back().size() == I.schema.x) I.merge_groups.push_back({});
     I.merge_groups.back().push_back(s.stripe_id);
     stripes_[s.stripe_id] = s;
@@ -650,12 +696,11 @@ bool Loopback::get(const std::string& key, std::vector<char>& value) {
     auto it = objects_.find(key);
     if (it == objects_.end()) return false;
     const Stripe& s = stripes_.at(it->second.first);
-    const int first = it->second.second;
-    const int k_obj = I.schema.ec_type == ECG_RS || I.schema.ec_type == ECG_ERS ? I.schema.cp.k : s.k;
+    const std::vector<int>& blocks = it->second.second;
     const size_t B = I.schema.block_size;
-    value.assign((size_t)k_obj * B, 0);
-    for (int j = 0; j < k_obj; j++) {
-        const int b = first + j;
+    value.assign(blocks.size() * B, 0);
+    for (size_t j = 0; j < blocks.size(); j++) {
+        const int b = blocks[j];
         if (!I.store.access_data(I.topo.node_port(s.blocks2nodes[b]), key_of(s.block_ids[b]), value.data() + j * B, B))
             return false;
     }
@@ -720,9 +765,14 @@ bool Loopback::repair(unsigned stripe_id, const std::vector<int>& failures) {
     return good;
 }
 
-bool Loopback::merge(int step_size) {  // merge.cpp:19-450 (RS family)
+bool Loopback::merge(int step_size) {  // Coordinator::do_stripe_merge (merge.cpp:5-17)
+    if (impl_->schema.ec_type == ECG_RS) return rs_merge(step_size);
+    if (impl_->schema.ec_type == ECG_PC || impl_->schema.ec_type == ECG_HV_PC) return pc_merge(step_size);
+    return false;
+}
+
+bool Loopback::rs_merge(int step_size) {  // merge.cpp:19-450
     Impl& I = *impl_;
-    if (I.schema.ec_type != ECG_RS) return false;
     const double t0 = now_s();
     const size_t B = I.schema.block_size;
     std::vector<std::vector<unsigned>> new_groups;
@@ -733,7 +783,7 @@ bool Loopback::merge(int step_size) {  // merge.cpp:19-450 (RS family)
             Stripe big;
             big.stripe_id = I.cur_stripe_id++;
             std::vector<unsigned> parity_nodes, old_parity_ids, old_parity_nodes;
-            std::vector<std::pair<int, std::vector<BlockLoc>>> clusters;  // in order of first data block
+            std::vector<BlockLoc> inputs;  // data blocks under their merged-stripe index seri * k + i
             int k0 = 0, m0 = 0;
             for (int seri = 0; seri < step_size; seri++) {
                 const Stripe& t = stripes_.at(group[mi + seri]);
@@ -744,13 +794,7 @@ bool Loopback::merge(int step_size) {  // merge.cpp:19-450 (RS family)
                     if (i < t.k) {
                         big.blocks2nodes.push_back(node);
                         big.block_ids.push_back(t.block_ids[i]);
-                        const int c = I.topo.cluster_of(node);
-                        auto it = std::find_if(clusters.begin(), clusters.end(), [&](auto& e) { return e.first == c; });
-                        if (it == clusters.end()) {
-                            clusters.push_back({c, {}});
-                            it = clusters.end() - 1;
-                        }
-                        it->second.push_back({seri * t.k + i, t.block_ids[i], node});
+                        inputs.push_back({seri * t.k + i, t.block_ids[i], node});
                     } else {
                         parity_nodes.push_back(node);
                         old_parity_ids.push_back(t.block_ids[i]);
@@ -768,41 +812,18 @@ bool Loopback::merge(int step_size) {  // merge.cpp:19-450 (RS family)
             main.cp = cp;
             main.block_size = B;
             main.partial_decoding = I.schema.partial_decoding;
-            int parity_cluster = 0;
-            for (int i = 0; i < m0; i++) {
+            for (int i = 0; i < m0; i++) {  // new parities on the first stripe's parity nodes
                 big.blocks2nodes.push_back(parity_nodes[i]);
                 big.block_ids.push_back(I.cur_block_id++);
-                parity_cluster = I.topo.cluster_of(parity_nodes[i]);
+                main.cluster_id = I.topo.cluster_of(parity_nodes[i]);
                 main.parity_idx.push_back(big.k + i);
                 main.new_parity_ids.push_back(big.block_ids.back());
                 main.new_nodes.push_back(parity_nodes[i]);
             }
-            main.cluster_id = parity_cluster;
             std::vector<RecalCall> helps;
-            for (auto& c : clusters) {
-                if (c.first == parity_cluster) {
-                    main.inner = c.second;
-                } else {
-                    RecalCall h = main;
-                    h.cluster_id = c.first;
-                    h.inner = c.second;
-                    h.help.clear();
-                    h.new_parity_ids.clear();
-                    h.new_nodes.clear();
-                    main.help.push_back(c.second);
-                    helps.push_back(h);
-                }
-            }
-            Channel chan;
-            std::vector<std::thread> threads;
-            std::vector<char> help_ok(helps.size(), 1);
-            for (size_t i = 0; i < helps.size(); i++)
-                threads.emplace_back([&, i] { help_ok[i] = I.help_recal(helps[i], chan); });
+            I.split_recal(main, inputs, helps);
             std::vector<Block> parities;
-            bool ok = I.main_recal(main, chan, parities);
-            for (auto& t : threads) t.join();
-            ok = ok && std::find(help_ok.begin(), help_ok.end(), 0) == help_ok.end();
-            if (!ok) {
+            if (!I.run_recal(main, helps, parities)) {
                 all_ok = false;
                 continue;
             }
@@ -819,7 +840,9 @@ bool Loopback::merge(int step_size) {  // merge.cpp:19-450 (RS family)
                 Stripe& t = stripes_.at(group[mi + seri]);
                 for (auto& key : t.objects) {
                     big.objects.push_back(key);
-                    objects_[key] = {big.stripe_id, seri * t.k};
+                    std::vector<int> blocks(t.k);
+                    for (int j = 0; j < t.k; j++) blocks[j] = seri * t.k + j;
+                    objects_[key] = {big.stripe_id, blocks};
                 }
                 ecg_ec_destroy(t.ec);
                 stripes_.erase(group[mi + seri]);
@@ -829,6 +852,112 @@ bool Loopback::merge(int step_size) {  // merge.cpp:19-450 (RS family)
             stripes_[big.stripe_id] = big;
             stats.merges++;
             stats.merged_parities += m0;
+        }
+    }
+    I.merge_groups = new_groups;
+    stats.merge_s += now_s() - t0;
+    return all_ok;
+}
+
+bool Loopback::pc_merge(int step_size) {  // merge.cpp:877-1505, multistripe rule HORIZONTAL
+    Impl& I = *impl_;
+    const double t0 = now_s();
+    const size_t B = I.schema.block_size;
+    const bool hv = I.schema.ec_type == ECG_HV_PC;
+    std::vector<std::vector<unsigned>> new_groups;
+    bool all_ok = true;
+    for (auto& group : I.merge_groups) {
+        if ((int)group.size() % step_size != 0) continue;
+        for (size_t mi = 0; mi < group.size(); mi += step_size) {
+            ecg_coding_parameters oc{};
+            ecg_ec_get_coding_parameters(stripes_.at(group[mi]).ec, &oc);
+            const int k1 = oc.k1, m1 = oc.m1, k2 = oc.k2, m2 = oc.m2, K1 = step_size * k1;
+            ecg_coding_parameters nc = oc;  // Coordinator::new_ec_for_merge: k1 *= x (auxs.cpp:113-117)
+            nc.k1 = K1;
+            nc.x = step_size;
+            Stripe big;
+            big.stripe_id = I.cur_stripe_id++;
+            big.ec = ecg_ec_factory(I.schema.ec_type, &nc);
+            if (!big.ec) return false;
+            ecg_ec_init_coding_parameters(big.ec, &nc);
+            ecg_ec_set_memory(big.ec, ECG_MEM_HOST, nullptr);
+            big.k = ecg_ec_k(big.ec);
+            big.m = ecg_ec_m(big.ec);
+            big.block_ids.assign(big.k + big.m, 0);
+            big.blocks2nodes.assign(big.k + big.m, 0);
+            const int rows = k2 + m2;
+            std::vector<std::vector<BlockLoc>> row_inputs(rows);
+            std::vector<std::vector<unsigned>> parity_nodes(rows, std::vector<unsigned>(m1, 0));
+            std::vector<std::pair<unsigned, unsigned>> old_parities;  // (node, block id)
+            for (int seri = 0; seri < step_size; seri++) {
+                const Stripe& t = stripes_.at(group[mi + seri]);
+                for (int i = 0; i < t.k + t.m; i++) {
+                    int row = -1, col = -1;
+                    ecg_ec_bid2rowcol(t.ec, i, &row, &col);
+                    if (col < k1) {  // data and column-parity blocks keep their place in the wider grid
+                        const int nb = ecg_ec_rowcol2bid(big.ec, row, seri * k1 + col);
+                        big.block_ids[nb] = t.block_ids[i];
+                        big.blocks2nodes[nb] = t.blocks2nodes[i];
+                        row_inputs[row].push_back({seri * k1 + col, t.block_ids[i], t.blocks2nodes[i]});
+                    } else {  // row parities and global parities are recomputed in place of the old ones
+                        parity_nodes[row][col - k1] = t.blocks2nodes[i];
+                        old_parities.push_back({t.blocks2nodes[i], t.block_ids[i]});
+                    }
+                }
+            }
+            bool ok = true;
+            for (int row = 0; row < rows && ok; row++) {
+                if (hv && row >= k2) continue;  // HVPC has no global parities (merge.cpp:1312-1321)
+                RecalCall main;
+                main.ec_type = ECG_RS;  // the row code RS(x * k1, m1)
+                main.cp.k = K1;
+                main.cp.m = m1;
+                main.cp.x = step_size;
+                main.block_size = B;
+                main.partial_decoding = I.schema.partial_decoding;
+                for (int ii = 0; ii < m1; ii++) {
+                    const int nb = ecg_ec_rowcol2bid(big.ec, row, K1 + ii);
+                    big.block_ids[nb] = I.cur_block_id++;
+                    big.blocks2nodes[nb] = parity_nodes[row][ii];
+                    main.parity_idx.push_back(K1 + ii);
+                    main.new_parity_ids.push_back(big.block_ids[nb]);
+                    main.new_nodes.push_back(parity_nodes[row][ii]);
+                    main.cluster_id = I.topo.cluster_of(parity_nodes[row][ii]);
+                }
+                std::vector<RecalCall> helps;
+                I.split_recal(main, row_inputs[row], helps);
+                std::vector<Block> parities;
+                ok = I.run_recal(main, helps, parities);
+                for (int ii = 0; ok && ii < m1; ii++)
+                    ok = I.store.store_data(I.topo.node_port(main.new_nodes[ii]), key_of(main.new_parity_ids[ii]),
+                                            parities[ii].data(), B);
+            }
+            if (!ok) {
+                all_ok = false;
+                ecg_ec_destroy(big.ec);
+                continue;
+            }
+            for (auto& op : old_parities) I.store.remove_data(I.topo.node_port(op.first), key_of(op.second));
+            for (int seri = 0; seri < step_size; seri++) {
+                Stripe& t = stripes_.at(group[mi + seri]);
+                for (auto& key : t.objects) {  // an object's data: its old grid, columns shifted by seri * k1
+                    big.objects.push_back(key);
+                    std::vector<int> blocks;
+                    for (int b : objects_.at(key).second) {
+                        int row = -1, col = -1;
+                        ecg_ec_bid2rowcol(t.ec, b, &row, &col);
+                        blocks.push_back(ecg_ec_rowcol2bid(big.ec, row, seri * k1 + col));
+                    }
+                    objects_[key] = {big.stripe_id, blocks};
+                }
+                ecg_ec_destroy(t.ec);
+                stripes_.erase(group[mi + seri]);
+            }
+            if (new_groups.empty() || (int)new_groups.back().size() == I.schema.x) new_groups.push_back({});
+            new_groups.back().push_back(big.stripe_id);
+            stripes_[big.stripe_id] = big;
+            stats.merges++;
+            stats.merged_parities += hv ? (long)k2 * m1 : (long)rows * m1;
         }
     }
     I.merge_groups = new_groups;
@@ -869,7 +998,10 @@ std::string Loopback::manifest_json() const {
         o << "], \"objects\": [";
         bool f2 = true;
         for (auto& key : s.objects) {
-            o << (f2 ? "" : ", ") << "[\"" << key << "\", " << objects_.at(key).second << "]";
+            o << (f2 ? "" : ", ") << "[\"" << key << "\", [";
+            const auto& blocks = objects_.at(key).second;
+            for (size_t j = 0; j < blocks.size(); j++) o << (j ? ", " : "") << blocks[j];
+            o << "]]";
             f2 = false;
         }
         o << "]}";

@@ -82,7 +82,7 @@ public:
     bool get(const std::string& key, std::vector<char>& value);
     // client.blocks_repair (repair.cpp:5-155): returns false if the code cannot repair the set
     bool repair(unsigned stripe_id, const std::vector<int>& failures);
-    // client.merge (merge.cpp:19-450): RS family only
+    // client.merge: RS (merge.cpp:19-450) and PC / HV_PC horizontal (merge.cpp:877-1505)
     bool merge(int step_size);
 
     std::vector<unsigned> list_stripes() const;
@@ -97,7 +97,10 @@ private:
     struct Impl;
     std::unique_ptr<Impl> impl_;
     std::map<unsigned, Stripe> stripes_;
-    std::unordered_map<std::string, std::pair<unsigned, int>> objects_;  // key -> (stripe, seri in stripe)
+    // key -> (stripe, the object's data blocks in value order)
+    std::unordered_map<std::string, std::pair<unsigned, std::vector<int>>> objects_;
+    bool rs_merge(int step_size);
+    bool pc_merge(int step_size);
     friend struct Impl;
 };
 

@@ -54,6 +54,38 @@ int rule_of(const std::string& s) {
     return -1;
 }
 
+// --selftest-store: the block stores alone (no GPU): store / access / overwrite / remove / batch / count
+int selftest_store(const std::string& kind, const std::string& dir) {
+    auto st = make_block_store(kind, dir);
+    if (!st) return 2;
+    const size_t B = 4096;
+    std::vector<int> ports;
+    std::vector<std::string> keys;
+    std::vector<char> staging(16 * B), back(16 * B);
+    for (int i = 0; i < 16; i++) {
+        ports.push_back(17600 + i % 5);
+        keys.push_back(std::to_string(1000 + i));
+    }
+    std::vector<char> v = object_bytes(3, 0, staging.size());
+    memcpy(staging.data(), v.data(), v.size());
+    int fails = 0;
+    fails += !st->store_batch(ports, keys, staging.data(), B);
+    fails += st->count() != 16;
+    fails += !st->access_batch(ports, keys, back.data(), B);
+    fails += staging != back;
+    std::vector<char> one(B, 7), got(B);
+    fails += !st->store_data(17600, keys[0], one.data(), B);  // overwrite
+    fails += !st->access_data(17600, keys[0], got.data(), B) || got != one;
+    fails += st->access_data(17601, keys[0], got.data(), B);  // other datanode: absent
+    fails += !st->remove_data(17600, keys[0]);
+    fails += st->access_data(17600, keys[0], got.data(), B);
+    fails += st->count() != 15;
+    for (int i = 1; i < 16; i++) fails += !st->remove_data(ports[i], keys[i]);
+    fails += st->count() != 0;
+    printf("{\"selftest_store\": \"%s\", \"failures\": %d}\n", kind.c_str(), fails);
+    return fails ? 1 : 0;
+}
+
 void usage() {
     fprintf(stderr,
             "ecg_loopback [--ec RS] [--k 6 --m 4 | --k --l --g | --k1 --m1 --k2 --m2] [--block-size 1024]\n"
@@ -100,6 +132,7 @@ int main(int argc, char** argv) {
         else if (a == "--multi") multi = atoi(val().c_str());
         else if (a == "--no-merge") do_merge = false;
         else if (a == "--manifest") manifest = val();
+        else if (a == "--selftest-store") return selftest_store(store_kind, dir);
         else {
             usage();
             return 2;
@@ -151,7 +184,7 @@ int main(int argc, char** argv) {
     long pre_single = 0, pre_multi = 0, post_single = 0, post_multi = 0;
     repairs(pre_single, pre_multi);
     bool merged = false;
-    if (do_merge && schema.ec_type == ECG_RS) {
+    if (do_merge && (schema.ec_type == ECG_RS || schema.ec_type == ECG_PC || schema.ec_type == ECG_HV_PC)) {
         merged = lb.merge(schema.x);
         repairs(post_single, post_multi);
     }

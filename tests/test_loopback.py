@@ -29,6 +29,18 @@ def test_cli_usage_errors():
     assert p.returncode == 2
 
 
+@pytest.mark.parametrize("kind", ["kv", "disk"])
+def test_block_store_selftest(tmp_path, kind):
+    """Datanode block stores (datanode.cpp:64-169) without a GPU: batch store/access through one staging
+    buffer, overwrite, per-datanode key spaces, removal, counts; the disk layout is <dir>/<port>/<id>."""
+    p = subprocess.run([BIN, "--store", kind, "--dir", str(tmp_path / "st"), "--selftest-store"],
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert json.loads(p.stdout.strip().splitlines()[-1])["failures"] == 0
+    if kind == "disk":
+        assert sorted(os.listdir(tmp_path / "st")) == [str(17600 + i) for i in range(5)]
+
+
 def _objects(seed, k, B, n):
     from oracle import ref
     return [ref.splitmix_bytes(seed, j * k * B // 8, k * B) for j in range(n)]
@@ -69,9 +81,9 @@ def test_config1_disk_store_vs_oracle(tmp_path, oracle):
         par = [np.zeros(B, np.uint8) for _ in range(mm)]
         oracle.jerasure_matrix_encode(k, mm, M, blocks[:k], par, B)
         assert all(np.array_equal(a, b) for a, b in zip(par, blocks[k:])), st["id"]
-        for key, first in st["objects"]:
-            j = int(key[3:])
-            assert np.array_equal(np.concatenate(blocks[first:first + 6]), objs[j]), key
+        for key, idxs in st["objects"]:
+            assert idxs == list(range(idxs[0], idxs[0] + 6))  # RS merge: objects stay contiguous
+            assert np.array_equal(np.concatenate([blocks[i] for i in idxs]), objs[int(key[3:])]), key
 
 
 @pytest.mark.gpu
@@ -81,6 +93,39 @@ def test_config1_without_partial_decoding():
     assert rc == 0, p.stdout + p.stderr
     assert s["plans_partial"] == 0 and s["plans_direct"] > 0 and s["helper_messages"] == 0
     assert s["rebuilt_mismatch"] == 0 and s["gets_ok"] == 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("code,params", [
+    ("PC", dict(k1=4, m1=1, k2=4, m2=1)),      # BASELINE config 4's code
+    ("HV_PC", dict(k1=4, m1=2, k2=2, m2=1)),
+    ("PC", dict(k1=3, m1=2, k2=2, m2=2)),
+])
+def test_pc_merge_vs_oracle(tmp_path, oracle, code, params):
+    """Config 4's call path: x = 2 horizontal merge (merge.cpp:877-1505 -> main_recal / help_recal) with
+    partial encoding per row, then repairs on the merged PC(2*k1, m1, k2, m2); the final disk store must
+    equal the oracle's product-code encoding of each merged grid, and every object its bytes."""
+    from oracle import ec_ref as E
+    store, man = tmp_path / "storage", tmp_path / "manifest.json"
+    args = ["--ec", code] + sum([[f"--{k}", str(v)] for k, v in params.items()], [])
+    rc, s, p = run(args + ["--block-size", "4096", "--stripes", "8", "--multi", "3", "--store", "disk",
+                           "--dir", str(store), "--seed", "11", "--manifest", str(man)])
+    assert rc == 0, p.stdout + p.stderr
+    assert s["merged"] and s["merges"] == 4 and s["final_stripes"] == 4 and s["rebuilt_mismatch"] == 0
+    m = json.load(open(man))
+    B = m["block_size"]
+    k = params["k1"] * params["k2"]
+    objs = _objects(11, k, B, 8)
+    for st in m["stripes"]:
+        cp = {kk: st["cp"][kk] for kk in ("k1", "m1", "k2", "m2")}
+        assert cp["k1"] == 2 * params["k1"]
+        blocks = [np.fromfile(store / str(port) / str(bid), dtype=np.uint8) for bid, port in st["blocks"]]
+        ec = E.ec_factory(E.ECTYPE[code], E.CodingParameters(**cp))
+        par = E.zeros(ec.m, B)
+        ec.encode(blocks[:ec.k], par, B)
+        assert all(np.array_equal(a, b) for a, b in zip(par, blocks[ec.k:])), st["id"]
+        for key, idxs in st["objects"]:
+            assert np.array_equal(np.concatenate([blocks[i] for i in idxs]), objs[int(key[3:])]), key
 
 
 def _gf_rank(rows, oracle):
