@@ -367,8 +367,8 @@ struct Loopback::Impl {
             main.cp.k = plan.local_or_column ? k2 : k1;
             main.cp.m = plan.local_or_column ? m2 : m1;
             main.ec_type = ECG_RS;
-            if (schema.ec_type == ECG_HIERACHICAL_PC)  // multistripe rule RAND: isvertical = false
-                main.ec_type = plan.local_or_column ? ECG_RS : ECG_ERS;
+            if (schema.ec_type == ECG_HIERACHICAL_PC)  // HPC objects are vertical (pc.h:66): ERS columns
+                main.ec_type = plan.local_or_column ? ECG_ERS : ECG_RS;  // repair.cpp:393-409
         } else {
             main.cp = scp;
             main.ec_type = schema.ec_type;
@@ -496,6 +496,14 @@ struct Loopback::Impl {
         const size_t B = p.block_size;
         Ec ec(p.ec_type, p.cp);
         if (!ec.h) return false;
+        if (p.ec_type == ECG_HIERACHICAL_PC) {  // :100-157: new parity = XOR of the old ones (ERS rows)
+            std::vector<Block> old(p.inner.size());
+            for (size_t i = 0; i < p.inner.size(); i++)
+                if (!read(p.inner[i], B, old[i])) return false;
+            out.assign(np, Block(B, 0));
+            auto dp = ptrs(old), op = ptrs(out);
+            return ok(ecg_ec_perform_addition(ec.h, dp.data(), op.data(), (int)B, (int)old.size(), np));
+        }
         std::vector<Block> orig;
         std::vector<int> orig_idx;
         auto take = [&](const BlockLoc& b) {
@@ -768,7 +776,9 @@ bool Loopback::repair(unsigned stripe_id, const std::vector<int>& failures) {
 bool Loopback::merge(int step_size) {  // Coordinator::do_stripe_merge (merge.cpp:5-17)
     if (impl_->schema.ec_type == ECG_RS) return rs_merge(step_size);
     if (impl_->schema.ec_type == ECG_PC || impl_->schema.ec_type == ECG_HV_PC) return pc_merge(step_size);
-    return false;
+    if (impl_->schema.ec_type == ECG_HIERACHICAL_PC) return hpc_merge(step_size);
+    if (impl_->schema.ec_type == ECG_AZURE_LRC) return lrc_merge(step_size);
+    return false;  // do_stripe_merge has no path for the other LRCs (merge.cpp:7-16)
 }
 
 bool Loopback::rs_merge(int step_size) {  // merge.cpp:19-450
@@ -859,7 +869,8 @@ bool Loopback::rs_merge(int step_size) {  // merge.cpp:19-450
     return all_ok;
 }
 
-bool Loopback::pc_merge(int step_size) {  // merge.cpp:877-1505, multistripe rule HORIZONTAL
+// merge.cpp:877-1505 (PC, HVPC), multistripe rule HORIZONTAL
+bool Loopback::pc_merge(int step_size) {
     Impl& I = *impl_;
     const double t0 = now_s();
     const size_t B = I.schema.block_size;
@@ -958,6 +969,204 @@ bool Loopback::pc_merge(int step_size) {  // merge.cpp:877-1505, multistripe rul
             stripes_[big.stripe_id] = big;
             stats.merges++;
             stats.merged_parities += hv ? (long)k2 * m1 : (long)rows * m1;
+        }
+    }
+    I.merge_groups = new_groups;
+    stats.merge_s += now_s() - t0;
+    return all_ok;
+}
+
+bool Loopback::lrc_merge(int step_size) {  // azu_lrc_merge, merge.cpp:451-877
+    Impl& I = *impl_;
+    const double t0 = now_s();
+    const size_t B = I.schema.block_size;
+    std::vector<std::vector<unsigned>> new_groups;
+    bool all_ok = true;
+    for (auto& group : I.merge_groups) {
+        if ((int)group.size() % step_size != 0) continue;
+        for (size_t mi = 0; mi < group.size(); mi += step_size) {
+            ecg_coding_parameters oc{};
+            ecg_ec_get_coding_parameters(stripes_.at(group[mi]).ec, &oc);
+            const int k = oc.k, l = oc.l, g = oc.g;
+            ecg_coding_parameters nc = oc;  // new_ec_for_merge: k *= x, l *= x (auxs.cpp:109-111)
+            nc.k = step_size * k;
+            nc.l = step_size * l;
+            nc.m = nc.l + g;
+            nc.x = step_size;
+            nc.local_or_column = 0;
+            Stripe big;
+            big.stripe_id = I.cur_stripe_id++;
+            big.ec = ecg_ec_factory(I.schema.ec_type, &nc);
+            if (!big.ec) return false;
+            ecg_ec_init_coding_parameters(big.ec, &nc);
+            ecg_ec_set_memory(big.ec, ECG_MEM_HOST, nullptr);
+            big.k = ecg_ec_k(big.ec);
+            big.m = ecg_ec_m(big.ec);
+            big.block_ids.assign(big.k + big.m, 0);
+            big.blocks2nodes.assign(big.k + big.m, 0);
+            std::vector<BlockLoc> inputs;
+            std::vector<unsigned> parity_nodes;
+            std::vector<std::pair<unsigned, unsigned>> old_globals;
+            for (int seri = 0; seri < step_size; seri++) {
+                const Stripe& t = stripes_.at(group[mi + seri]);
+                for (int i = 0; i < t.k + t.m; i++) {
+                    if (i < k || i >= k + g) {  // data and local parities keep their blocks
+                        const int ni = i < k ? seri * k + i : big.k + g + seri * l + (i - k - g);
+                        big.block_ids[ni] = t.block_ids[i];
+                        big.blocks2nodes[ni] = t.blocks2nodes[i];
+                        if (i < k) inputs.push_back({ni, t.block_ids[i], t.blocks2nodes[i]});
+                    } else {
+                        parity_nodes.push_back(t.blocks2nodes[i]);
+                        old_globals.push_back({t.blocks2nodes[i], t.block_ids[i]});
+                    }
+                }
+            }
+            RecalCall main;
+            main.ec_type = I.schema.ec_type;
+            main.cp = nc;
+            main.block_size = B;
+            main.partial_decoding = I.schema.partial_decoding;
+            for (int j = 0; j < g; j++) {  // the globals land on the first stripe's global nodes
+                big.block_ids[big.k + j] = I.cur_block_id++;
+                big.blocks2nodes[big.k + j] = parity_nodes[j];
+                main.cluster_id = I.topo.cluster_of(parity_nodes[j]);
+                main.parity_idx.push_back(big.k + j);
+                main.new_parity_ids.push_back(big.block_ids[big.k + j]);
+                main.new_nodes.push_back(parity_nodes[j]);
+            }
+            std::vector<RecalCall> helps;
+            I.split_recal(main, inputs, helps);
+            std::vector<Block> parities;
+            bool ok = I.run_recal(main, helps, parities);
+            for (int j = 0; ok && j < g; j++)
+                ok = I.store.store_data(I.topo.node_port(main.new_nodes[j]), key_of(main.new_parity_ids[j]),
+                                        parities[j].data(), B);
+            if (!ok) {
+                all_ok = false;
+                ecg_ec_destroy(big.ec);
+                continue;
+            }
+            for (auto& og : old_globals) I.store.remove_data(I.topo.node_port(og.first), key_of(og.second));
+            for (int seri = 0; seri < step_size; seri++) {
+                Stripe& t = stripes_.at(group[mi + seri]);
+                for (auto& key : t.objects) {
+                    big.objects.push_back(key);
+                    std::vector<int> blocks;
+                    for (int b : objects_.at(key).second) blocks.push_back(seri * k + b);
+                    objects_[key] = {big.stripe_id, blocks};
+                }
+                ecg_ec_destroy(t.ec);
+                stripes_.erase(group[mi + seri]);
+            }
+            if (new_groups.empty() || (int)new_groups.back().size() == I.schema.x) new_groups.push_back({});
+            new_groups.back().push_back(big.stripe_id);
+            stripes_[big.stripe_id] = big;
+            stats.merges++;
+            stats.merged_parities += g;
+        }
+    }
+    I.merge_groups = new_groups;
+    stats.merge_s += now_s() - t0;
+    return all_ok;
+}
+
+// hpc_merge (merge.cpp:1505-1905), multistripe rule VERTICAL: HPC columns are ERS(k2, m2, x, seri)
+// slices of one Vandermonde(x * k2, m2), so a merged column parity is the XOR of the x old ones, read
+// by the parity's proxy (handle_merge.cpp:100-157); rows (data and row parities) keep their blocks.
+bool Loopback::hpc_merge(int step_size) {
+    Impl& I = *impl_;
+    const double t0 = now_s();
+    const size_t B = I.schema.block_size;
+    std::vector<std::vector<unsigned>> new_groups;
+    bool all_ok = true;
+    for (auto& group : I.merge_groups) {
+        if ((int)group.size() % step_size != 0) continue;
+        for (size_t mi = 0; mi < group.size(); mi += step_size) {
+            ecg_coding_parameters oc{};
+            ecg_ec_get_coding_parameters(stripes_.at(group[mi]).ec, &oc);
+            const int k1 = oc.k1, m1 = oc.m1, k2 = oc.k2, m2 = oc.m2, K2 = step_size * k2;
+            ecg_coding_parameters nc = oc;  // new_ec_for_merge, VERTICAL: k2 *= x (auxs.cpp:113-115)
+            nc.k2 = K2;
+            nc.x = step_size;
+            Stripe big;
+            big.stripe_id = I.cur_stripe_id++;
+            big.ec = ecg_ec_factory(ECG_HIERACHICAL_PC, &nc);
+            if (!big.ec) return false;
+            ecg_ec_init_coding_parameters(big.ec, &nc);
+            ecg_ec_set_memory(big.ec, ECG_MEM_HOST, nullptr);
+            big.k = ecg_ec_k(big.ec);
+            big.m = ecg_ec_m(big.ec);
+            big.block_ids.assign(big.k + big.m, 0);
+            big.blocks2nodes.assign(big.k + big.m, 0);
+            const int cols = k1 + m1;
+            std::vector<std::vector<BlockLoc>> old_col_parities(cols);
+            std::vector<std::vector<unsigned>> parity_nodes(cols, std::vector<unsigned>(m2, 0));
+            std::vector<std::pair<unsigned, unsigned>> old_parities;
+            for (int seri = 0; seri < step_size; seri++) {
+                const Stripe& t = stripes_.at(group[mi + seri]);
+                for (int i = 0; i < t.k + t.m; i++) {
+                    int row = -1, col = -1;
+                    ecg_ec_bid2rowcol(t.ec, i, &row, &col);
+                    if (row < k2) {  // data and row parities: rows stack (oldbid2newbid_for_merge, pc.cpp:361-376)
+                        const int nb = ecg_ec_rowcol2bid(big.ec, seri * k2 + row, col);
+                        big.block_ids[nb] = t.block_ids[i];
+                        big.blocks2nodes[nb] = t.blocks2nodes[i];
+                    } else {
+                        parity_nodes[col][row - k2] = t.blocks2nodes[i];
+                        old_parities.push_back({t.blocks2nodes[i], t.block_ids[i]});
+                        old_col_parities[col].push_back({seri * m2 + row - k2, t.block_ids[i], t.blocks2nodes[i]});
+                    }
+                }
+            }
+            bool ok = true;
+            for (int col = 0; col < cols && ok; col++) {
+                RecalCall main;
+                main.ec_type = ECG_HIERACHICAL_PC;
+                main.cp = nc;
+                main.block_size = B;
+                main.partial_decoding = I.schema.partial_decoding;
+                main.inner = old_col_parities[col];
+                for (int ii = 0; ii < m2; ii++) {
+                    const int nb = ecg_ec_rowcol2bid(big.ec, K2 + ii, col);
+                    big.block_ids[nb] = I.cur_block_id++;
+                    big.blocks2nodes[nb] = parity_nodes[col][ii];
+                    main.parity_idx.push_back(K2 + ii);
+                    main.new_parity_ids.push_back(big.block_ids[nb]);
+                    main.new_nodes.push_back(parity_nodes[col][ii]);
+                    main.cluster_id = I.topo.cluster_of(parity_nodes[col][ii]);
+                }
+                std::vector<Block> parities;
+                ok = I.run_recal(main, {}, parities);
+                for (int ii = 0; ok && ii < m2; ii++)
+                    ok = I.store.store_data(I.topo.node_port(main.new_nodes[ii]), key_of(main.new_parity_ids[ii]),
+                                            parities[ii].data(), B);
+            }
+            if (!ok) {
+                all_ok = false;
+                ecg_ec_destroy(big.ec);
+                continue;
+            }
+            for (auto& op : old_parities) I.store.remove_data(I.topo.node_port(op.first), key_of(op.second));
+            for (int seri = 0; seri < step_size; seri++) {
+                Stripe& t = stripes_.at(group[mi + seri]);
+                for (auto& key : t.objects) {
+                    big.objects.push_back(key);
+                    std::vector<int> blocks;
+                    for (int b : objects_.at(key).second) {
+                        int row = -1, col = -1;
+                        ecg_ec_bid2rowcol(t.ec, b, &row, &col);
+                        blocks.push_back(ecg_ec_rowcol2bid(big.ec, seri * k2 + row, col));
+                    }
+                    objects_[key] = {big.stripe_id, blocks};
+                }
+                ecg_ec_destroy(t.ec);
+                stripes_.erase(group[mi + seri]);
+            }
+            if (new_groups.empty() || (int)new_groups.back().size() == I.schema.x) new_groups.push_back({});
+            new_groups.back().push_back(big.stripe_id);
+            stripes_[big.stripe_id] = big;
+            stats.merges++;
+            stats.merged_parities += (long)cols * m2;
         }
     }
     I.merge_groups = new_groups;

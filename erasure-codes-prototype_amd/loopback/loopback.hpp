@@ -82,7 +82,7 @@ public:
     bool get(const std::string& key, std::vector<char>& value);
     // client.blocks_repair (repair.cpp:5-155): returns false if the code cannot repair the set
     bool repair(unsigned stripe_id, const std::vector<int>& failures);
-    // client.merge: RS (merge.cpp:19-450) and PC / HV_PC horizontal (merge.cpp:877-1505)
+    // client.merge: RS, Azure LRC, PC / HVPC / HPC (horizontal), as do_stripe_merge dispatches them
     bool merge(int step_size);
 
     std::vector<unsigned> list_stripes() const;
@@ -100,7 +100,9 @@ private:
     // key -> (stripe, the object's data blocks in value order)
     std::unordered_map<std::string, std::pair<unsigned, std::vector<int>>> objects_;
     bool rs_merge(int step_size);
-    bool pc_merge(int step_size);
+    bool pc_merge(int step_size);   // PC / HVPC (merge.cpp:877-1505), horizontal
+    bool hpc_merge(int step_size);  // HPC (merge.cpp:1505-1905), vertical
+    bool lrc_merge(int step_size);  // Azure LRC (merge.cpp:451-877)
     friend struct Impl;
 };
 

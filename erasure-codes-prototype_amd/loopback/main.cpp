@@ -184,9 +184,13 @@ int main(int argc, char** argv) {
     long pre_single = 0, pre_multi = 0, post_single = 0, post_multi = 0;
     repairs(pre_single, pre_multi);
     bool merged = false;
-    if (do_merge && (schema.ec_type == ECG_RS || schema.ec_type == ECG_PC || schema.ec_type == ECG_HV_PC)) {
+    const bool mergeable = schema.ec_type == ECG_RS || schema.ec_type == ECG_AZURE_LRC || schema.ec_type >= ECG_PC;
+    if (do_merge && mergeable) {
         merged = lb.merge(schema.x);
-        repairs(post_single, post_multi);
+        // A merged HPC stripe's rows are RS(x*k1, m1) while the coordinator keeps addressing them as
+        // ERS(k1', m1, x, seri) (repair.cpp:393-409), so post-merge HPC repairs would use the wrong
+        // matrix in the reference; they are not run.
+        if (schema.ec_type != ECG_HIERACHICAL_PC) repairs(post_single, post_multi);
     }
     // get
     long get_ok = 0;

@@ -95,32 +95,51 @@ def test_config1_without_partial_decoding():
     assert s["rebuilt_mismatch"] == 0 and s["gets_ok"] == 8
 
 
+def _merged(code, params):
+    """(oracle class, merged parameters) of an x = 2 merge (Coordinator::new_ec_for_merge, auxs.cpp:102-120)."""
+    p = dict(params)
+    if code == "RS":
+        return "RS", dict(k=2 * p["k"], m=p["m"])
+    if code == "AZURE_LRC":
+        return "AZURE_LRC", dict(k=2 * p["k"], l=2 * p["l"], g=p["g"])
+    if code == "Hierachical_PC":  # vertical; merged columns are full Vandermonde(2*k2, m2): a plain PC
+        return "PC", dict(p, k2=2 * p["k2"])
+    return code, dict(p, k1=2 * p["k1"])  # PC / HV_PC, horizontal
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("code,params", [
     ("PC", dict(k1=4, m1=1, k2=4, m2=1)),      # BASELINE config 4's code
     ("HV_PC", dict(k1=4, m1=2, k2=2, m2=1)),
     ("PC", dict(k1=3, m1=2, k2=2, m2=2)),
+    ("AZURE_LRC", dict(k=12, l=2, g=2)),
+    ("AZURE_LRC", dict(k=6, l=2, g=2)),
+    ("Hierachical_PC", dict(k1=3, m1=1, k2=2, m2=2)),
 ])
-def test_pc_merge_vs_oracle(tmp_path, oracle, code, params):
-    """Config 4's call path: x = 2 horizontal merge (merge.cpp:877-1505 -> main_recal / help_recal) with
-    partial encoding per row, then repairs on the merged PC(2*k1, m1, k2, m2); the final disk store must
-    equal the oracle's product-code encoding of each merged grid, and every object its bytes."""
+def test_merge_vs_oracle(tmp_path, oracle, code, params):
+    """Stripe merging x = 2 as do_stripe_merge dispatches it (merge.cpp:5-17): PC / HVPC horizontal by
+    per-row partial encoding (config 4's call path), Azure LRC by global partial encoding, HPC vertical by
+    XOR of the old ERS column parities; then repairs on the merged stripes (not for HPC, see main.cpp).
+    The final disk store must equal the oracle's encoding of each merged stripe and every object its bytes."""
     from oracle import ec_ref as E
     store, man = tmp_path / "storage", tmp_path / "manifest.json"
     args = ["--ec", code] + sum([[f"--{k}", str(v)] for k, v in params.items()], [])
     rc, s, p = run(args + ["--block-size", "4096", "--stripes", "8", "--multi", "3", "--store", "disk",
                            "--dir", str(store), "--seed", "11", "--manifest", str(man)])
-    assert rc == 0, p.stdout + p.stderr
-    assert s["merged"] and s["merges"] == 4 and s["final_stripes"] == 4 and s["rebuilt_mismatch"] == 0
+    assert s["merged"] and s["merges"] == 4 and s["final_stripes"] == 4, p.stdout + p.stderr
+    assert s["ecg_errors"] == 0 and s["get_mismatch"] == 0 and s["gets_ok"] == 8
+    for mm in s["mismatches"]:  # LRC repairs: only reference-undecodable patterns may mismatch
+        assert code == "AZURE_LRC" and _undecodable(code, _merged(code, params)[1] if mm["stripe"] >= 8 else params,
+                                                     mm["failures"], oracle), mm
     m = json.load(open(man))
     B = m["block_size"]
-    k = params["k1"] * params["k2"]
-    objs = _objects(11, k, B, 8)
+    k_obj = params["k"] if "k" in params else params["k1"] * params["k2"]
+    objs = _objects(11, k_obj, B, 8)
+    ocode, mp = _merged(code, params)
     for st in m["stripes"]:
-        cp = {kk: st["cp"][kk] for kk in ("k1", "m1", "k2", "m2")}
-        assert cp["k1"] == 2 * params["k1"]
         blocks = [np.fromfile(store / str(port) / str(bid), dtype=np.uint8) for bid, port in st["blocks"]]
-        ec = E.ec_factory(E.ECTYPE[code], E.CodingParameters(**cp))
+        ec = E.ec_factory(E.ECTYPE[ocode], E.CodingParameters(**mp))
+        assert ec.k + ec.m == len(blocks)
         par = E.zeros(ec.m, B)
         ec.encode(blocks[:ec.k], par, B)
         assert all(np.array_equal(a, b) for a, b in zip(par, blocks[ec.k:])), st["id"]
@@ -171,6 +190,7 @@ def _params(args):
     ("UNIFORM_CAUCHY_LRC", ["--k", "8", "--l", "2", "--g", "2"]),
     ("PC", ["--k1", "4", "--m1", "1", "--k2", "4", "--m2", "1"]),
     ("HV_PC", ["--k1", "4", "--m1", "2", "--k2", "2", "--m2", "1"]),
+    ("Hierachical_PC", ["--k1", "3", "--m1", "1", "--k2", "2", "--m2", "2"]),
     ("RS", ["--k", "10", "--m", "4", "--placement", "RANDOM"]),
     ("RS", ["--k", "6", "--m", "3", "--placement", "FLAT"]),
 ])
@@ -188,13 +208,17 @@ def test_other_codes_repair_and_get(code, args, partial, oracle):
       * decode_local passes failed_num as row_k_ones (lrc.cpp:66-67), so a direct (non-partial) local
         decode of the Cauchy LRCs, whose group rows are not all ones, takes Jerasure's XOR-only "last
         drive" shortcut and rebuilds wrong bytes — in the reference too (the engine reproduces it
-        bit-exactly, tests/test_gpu_parity.py::test_cauchy_local_decode_quirk)."""
+        bit-exactly, tests/test_gpu_parity.py::test_cauchy_local_decode_quirk);
+      * EnlargedRSCode does not override decode, so RSCode::decode (rs.cpp:27-42) decodes an HPC's ERS
+        column with the plain Vandermonde matrix: a direct column repair of an HPC rebuilds wrong bytes in
+        the reference (the partial path uses make_encoding_matrix and is right)."""
     rc, s, p = run(["--ec", code] + args + ["--stripes", "6", "--multi", "4", "--partial", partial, "--no-merge"])
     assert s["ecg_errors"] == 0 and s["get_mismatch"] == 0 and s["gets_ok"] == 6, p.stdout + p.stderr
     assert s["repairs_failed"] == s["decode_undecodable"] and s["blocks_rebuilt"] > 0
     params = _params(args)
     for mm in s["mismatches"]:
         cauchy_quirk = code in ("OPTIMAL_CAUCHY_LRC", "UNIFORM_CAUCHY_LRC") and "direct-local" in mm["plans"]
-        assert cauchy_quirk or _undecodable(code, params, mm["failures"], oracle), mm
-    if code in ("RS", "PC", "HV_PC"):
+        ers_quirk = code == "Hierachical_PC" and "direct-local" in mm["plans"]
+        assert cauchy_quirk or ers_quirk or _undecodable(code, params, mm["failures"], oracle), mm
+    if code in ("RS", "PC", "HV_PC") or (code == "Hierachical_PC" and partial == "1"):
         assert s["rebuilt_mismatch"] == 0 and s["decode_undecodable"] == 0, s["mismatches"]
