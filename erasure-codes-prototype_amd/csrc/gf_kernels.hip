@@ -150,7 +150,16 @@ __device__ __forceinline__ void fold(const uint32_t (&x)[U][4], const ECG_CONST 
     else fold_general<MT, U>(x, t, acc);
 }
 
-constexpr int occupancy_for(int MT) { return MT <= 4 ? 6 : 4; }
+// Minimum waves per EU the register allocator must allow (r01 sweep, tools/gpu_variants.sh): 8 for the
+// 1-2-output kernels (decode, repair, XOR: +2 % at 8 vs 6), 6 for 3-4 outputs (encode: 8 costs 1 %),
+// 4 above.  ECG_OCC_OVERRIDE is for tuning builds only.
+constexpr int occupancy_for(int MT) {
+#ifdef ECG_OCC_OVERRIDE
+    return MT <= 4 ? ECG_OCC_OVERRIDE : 4;
+#else
+    return MT <= 2 ? 8 : MT <= 4 ? 6 : 4;
+#endif
+}
 
 // Workgroup -> (stripe, column chunk).  grid_map 0: linear (workgroup b takes chunk b).  grid_map 1:
 // XCD-contiguous -- the dispatcher deals workgroups round-robin over the 8 XCDs, so b % 8 names the

@@ -54,7 +54,7 @@ def main():
     enc_bytes = S * n * B
     dec_bytes = S * (k + 1) * B
 
-    def opt(nt=3, cpw=0, spec=0, gmap=1):
+    def opt(nt=3, cpw=0, spec=0, gmap=3):
         def f():  # spec: historical argument (compile-time-k kernels were removed after r01)
             ecg.set_option(ecg.ECG_OPT_NT, nt)
             ecg.set_option(ecg.ECG_OPT_COLS_PER_WG, cpw)
@@ -67,13 +67,20 @@ def main():
         halfS = S * n // 2
         src1, dst1 = flat[:halfS], flat[halfS:2 * halfS]
         variants += [
-            ("encode RS(10,4) defaults", opt(3, 0, 0, 1), lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes),
-            ("decode rot14 defaults", opt(3, 0, 0, 1),
+            ("encode RS(10,4) defaults", opt(3, 0, 0, 3), lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes),
+            ("decode rot14 defaults", opt(3, 0, 0, 3),
              lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=rebuilt, pattern_of_stripe=pos), dec_bytes),
-            ("copy 1->1 defaults", opt(3, 0, 0, 1), lambda: ecg.perform_addition_batch(1, 1, src1, dst1),
+            ("copy 1->1 defaults", opt(3, 0, 0, 3), lambda: ecg.perform_addition_batch(1, 1, src1, dst1),
              2 * halfS * B),
-            ("xor 10->1 defaults", opt(3, 0, 0, 1), lambda: ecg.perform_addition_batch(10, 1, data, rebuilt),
+            ("xor 10->1 defaults", opt(3, 0, 0, 3), lambda: ecg.perform_addition_batch(10, 1, data, rebuilt),
              S * 11 * B)]
+        variants += [
+            ("decode rot14 in-place defaults", opt(3, 0, 0, 3),
+             lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=None, pattern_of_stripe=pos), dec_bytes),
+            ("decode rot14 in-place map=1", opt(3, 0, 0, 1),
+             lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=None, pattern_of_stripe=pos), dec_bytes),
+            ("decode rot14 in-place map=2", opt(3, 0, 0, 2),
+             lambda: ecg.decode_batch(k, m, M, 1, pats, stripes, out=None, pattern_of_stripe=pos), dec_bytes)]
         for gmap in (1, 2):
             variants += [
                 (f"encode map={gmap}", opt(3, 0, 0, gmap), lambda: ecg.encode_batch(k, m, M, data, coding), enc_bytes),
