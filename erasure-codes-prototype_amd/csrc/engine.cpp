@@ -40,6 +40,10 @@ struct ThreadCtx {
     bool pipe_ready = false;
     uint8_t* pslot = nullptr;
     size_t pslot_cap = 0;
+    // small host calls: one pinned staging area mirroring the device scratch
+    uint8_t* pinned = nullptr;      // host view
+    uint8_t* pinned_dev = nullptr;  // device view (mapped, fine-grained)
+    size_t pinned_cap = 0;
     ~ThreadCtx() {
         // Process teardown may already have destroyed the runtime; leak rather than fault.
     }
@@ -244,24 +248,39 @@ int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks,
     return ECG_OK;
 }
 
+// Host-buffer tier (the reference's per-stripe calls on host memory).  Device slots are assigned to the
+// blocks that must be uploaded first (read before any op writes them), then to the rest, so the
+// inputs form one contiguous range.  Small calls (the proxy's 1 KiB - 64 KiB blocks) gather those
+// inputs into a per-thread pinned staging area with memcpy and move them with ONE H2D copy, and bring
+// every written block back with ONE D2H copy: two DMA transfers per call instead of one pageable copy
+// per block (each pageable copy is a driver-staged round trip).  Large calls copy block by block.
 int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B) {
     if (B < 0) return ECG_EINVAL;
     if (ops.empty() || B == 0) return ECG_OK;
     hipStream_t st = thread_stream();
     if (!st) return ECG_EHIP;
-    // Slots for every referenced block.
-    std::vector<int> slot(nblocks, -1);
-    int nslots = 0;
-    for (const LinearOp& op : ops) {
-        for (int id : op.src_ids) {
-            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
-            if (slot[id] < 0) slot[id] = nslots++;
-        }
-        for (int id : op.dst_ids) {
-            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
-            if (slot[id] < 0) slot[id] = nslots++;
+    std::vector<char> upload(nblocks, 0), written(nblocks, 0), used(nblocks, 0);
+    {
+        std::vector<char> produced(nblocks, 0);
+        for (const LinearOp& op : ops) {
+            for (int id : op.src_ids) {
+                if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+                if (!produced[id]) upload[id] = 1;
+                used[id] = 1;
+            }
+            for (int id : op.dst_ids) {
+                if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+                produced[id] = written[id] = used[id] = 1;
+            }
         }
     }
+    std::vector<int> slot(nblocks, -1);
+    int nslots = 0, n_up = 0;
+    for (int id = 0; id < nblocks; id++)
+        if (upload[id]) slot[id] = nslots++;
+    n_up = nslots;
+    for (int id = 0; id < nblocks; id++)
+        if (used[id] && slot[id] < 0) slot[id] = nslots++;
     const size_t pitch = ((size_t)B + 255) & ~(size_t)255;
     ThreadCtx& c = tctx(device_);
     if (c.cap < pitch * nslots) {
@@ -275,20 +294,69 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
     std::vector<uint8_t*> dev(nblocks, nullptr);
     for (int id = 0; id < nblocks; id++)
         if (slot[id] >= 0) dev[id] = c.scratch + (size_t)slot[id] * pitch;
-    std::vector<char> resident(nblocks, 0), written(nblocks, 0);
-    for (const LinearOp& op : ops) {
-        for (int id : op.src_ids) {
-            if (!resident[id]) {
-                ECG_HIP(hipMemcpyAsync(dev[id], blocks[id], (size_t)B, hipMemcpyHostToDevice, st));
-                resident[id] = 1;
+    const bool staged = (size_t)B <= kStagedMaxBlock && pitch * nslots <= kStagedMaxBytes;
+    if (staged && c.pinned_cap < pitch * nslots) {
+        ECG_HIP(hipStreamSynchronize(st));
+        if (c.pinned) (void)hipHostFree(c.pinned);
+        c.pinned = nullptr;
+        c.pinned_cap = 0;
+        const size_t cap = std::max(pitch * nslots, (size_t)1 << 20);
+        ECG_HIP(hipHostMalloc((void**)&c.pinned, cap, hipHostMallocMapped | hipHostMallocCoherent));
+        ECG_HIP(hipHostGetDevicePointer((void**)&c.pinned_dev, c.pinned, 0));
+        c.pinned_cap = cap;
+    }
+    // zero-copy: the kernel streams the (tiny) blocks straight over PCIe from / to the mapped staging area
+    const long long zc_max = get_option(ECG_OPT_ZEROCOPY_BYTES);
+    if (staged && zc_max > 0 && (long long)(pitch * nslots) <= zc_max) {
+        for (int id = 0; id < nblocks; id++) {
+            if (slot[id] < 0) continue;
+            dev[id] = c.pinned_dev + (size_t)slot[id] * pitch;
+            if (upload[id]) memcpy(c.pinned + (size_t)slot[id] * pitch, blocks[id], (size_t)B);
+        }
+        for (const LinearOp& op : ops) {
+            int rc = launch_one(op, dev.data(), B, st);
+            if (rc != ECG_OK) {
+                (void)hipStreamSynchronize(st);
+                return rc;
             }
         }
+        ECG_HIP(hipStreamSynchronize(st));
+        for (int id = 0; id < nblocks; id++)
+            if (written[id]) memcpy(blocks[id], c.pinned + (size_t)slot[id] * pitch, (size_t)B);
+        return ECG_OK;
+    }
+    if (staged) {
+        for (int id = 0; id < nblocks; id++)
+            if (upload[id]) memcpy(c.pinned + (size_t)slot[id] * pitch, blocks[id], (size_t)B);
+        if (n_up > 0) ECG_HIP(hipMemcpyAsync(c.scratch, c.pinned, pitch * n_up, hipMemcpyHostToDevice, st));
+    } else {
+        for (int id = 0; id < nblocks; id++)
+            if (upload[id]) ECG_HIP(hipMemcpyAsync(dev[id], blocks[id], (size_t)B, hipMemcpyHostToDevice, st));
+    }
+    for (const LinearOp& op : ops) {
         int rc = launch_one(op, dev.data(), B, st);
         if (rc != ECG_OK) {
             (void)hipStreamSynchronize(st);
             return rc;
         }
-        for (int id : op.dst_ids) resident[id] = written[id] = 1;
+    }
+    if (staged) {
+        int lo = nslots, hi = -1;
+        for (int id = 0; id < nblocks; id++)
+            if (written[id]) {
+                lo = std::min(lo, slot[id]);
+                hi = std::max(hi, slot[id]);
+            }
+        if (hi >= lo) {
+            ECG_HIP(hipMemcpyAsync(c.pinned + (size_t)lo * pitch, c.scratch + (size_t)lo * pitch,
+                                   (size_t)(hi - lo) * pitch + (size_t)B, hipMemcpyDeviceToHost, st));
+            ECG_HIP(hipStreamSynchronize(st));
+            for (int id = 0; id < nblocks; id++)
+                if (written[id]) memcpy(blocks[id], c.pinned + (size_t)slot[id] * pitch, (size_t)B);
+        } else {
+            ECG_HIP(hipStreamSynchronize(st));
+        }
+        return ECG_OK;
     }
     for (int id = 0; id < nblocks; id++)
         if (written[id]) ECG_HIP(hipMemcpyAsync(blocks[id], dev[id], (size_t)B, hipMemcpyDeviceToHost, st));

@@ -4,7 +4,8 @@
 //   run_device  - block pointers are device pointers (HBM-resident), asynchronous on a stream;
 //   run_host    - block pointers are host buffers (the reference's char** of host memory): blocks are
 //                 staged into per-thread device scratch, each block copied in at most once and every
-//                 written block copied back once, then the stream is synchronised;
+//                 written block copied back once, then the stream is synchronised; small calls gather
+//                 through a pinned staging area so a call costs one H2D and one D2H transfer;
 //   run_strided - batches of S stripes laid out as base + stripe/block strides, each stripe running
 //                 one of a small set of programs (e.g. 14 rotating single-erasure decode patterns).
 // Coefficient tables are built on the host once per distinct program set and cached in HBM.
@@ -24,6 +25,11 @@
 #include "matrix.hpp"
 
 namespace ecg {
+
+// run_host staging thresholds: calls with blocks up to 256 KiB and at most 8 MiB of scratch go
+// through the pinned staging area (memcpy + one DMA each way); larger ones copy block by block.
+constexpr size_t kStagedMaxBlock = 256 << 10;
+constexpr size_t kStagedMaxBytes = 8 << 20;
 
 struct ProgramSet {
     CoefTab* d_tabs = nullptr;

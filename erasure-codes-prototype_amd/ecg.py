@@ -35,7 +35,8 @@ ECG_EUNPINNED = -4
 ECG_OPT_NT = 0
 ECG_OPT_COLS_PER_WG = 1
 ECG_OPT_GRID_MAP = 2
-ECG_OPT_COUNT = 3
+ECG_OPT_ZEROCOPY_BYTES = 3
+ECG_OPT_COUNT = 4
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 

@@ -48,7 +48,10 @@ void ecg_free(void* p);            /* frees matrices returned by this library (m
 #define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 128; 0 = auto (128 = 2 KiB) */
 #define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous, 2 = stripe s on XCD group s%8,
                                   3 = auto (default): 1 when outputs live inside the input stripes, else 2 */
-#define ECG_OPT_COUNT 3
+#define ECG_OPT_ZEROCOPY_BYTES 3 /* host-buffer calls whose staged blocks total at most this many bytes
+                                    run the kernel on mapped pinned memory (no DMA); 0 = never;
+                                    default 1 MiB */
+#define ECG_OPT_COUNT 4
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

@@ -184,7 +184,7 @@ def test_bad_arguments(ecg):
 
 def test_tuning_options_validation(ecg):
     """ecg_set_option / ecg_get_option (include/ecg.h): range checks, defaults, no GPU needed."""
-    saved = [ecg.get_option(o) for o in range(3)]
+    saved = [ecg.get_option(o) for o in range(ecg.ECG_OPT_COUNT)]
     try:
         assert ecg.get_option(ecg.ECG_OPT_COUNT) == -1
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_NT, 4) != 0

@@ -512,6 +512,46 @@ def test_host_pipeline_encode_decode(ecg, oracle, torch_cuda, pinned):
     assert np.array_equal(h, orig)
 
 
+@pytest.mark.parametrize("zc", [0, 1 << 22])
+def test_host_tier_staging_paths(ecg, oracle, torch_cuda, zc):
+    """Host-buffer calls through the pinned staging area with DMA (zc = 0) or zero-copy kernels on the
+    mapped staging memory (ECG_OPT_ZEROCOPY_BYTES): encode, decode, wide pointer tables, multi-op plans."""
+    saved = ecg.get_option(ecg.ECG_OPT_ZEROCOPY_BYTES)
+    ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, zc)
+    try:
+        for k, m, B in [(6, 4, 1024), (10, 4, 4099), (130, 3, 256), (12, 4, 65536)]:
+            M = oracle.reed_sol_vandermonde_coding_matrix(k, m) if k + m <= 256 else None
+            data = [rnd(B, 7 * j + B) for j in range(k)]
+            a = [np.zeros(B, np.uint8) for _ in range(m)]
+            b = [np.full(B, 0x33, np.uint8) for _ in range(m)]
+            oracle.jerasure_matrix_encode(k, m, M, data, a, B)
+            ecg.jerasure_matrix_encode(k, m, M, data, b, B)
+            assert same(a, b), (k, m, B)
+            if k <= 12:
+                stripe = [x.copy() for x in data + a]
+                for e in (0, k - 1, k):
+                    S = [x.copy() for x in stripe]
+                    S[e][:] = 0
+                    assert ecg.jerasure_matrix_decode(k, m, M, 1, [e, -1], S[:k], S[k:], B) == 0
+                    assert same(S, stripe), (k, e)
+        # a product code decode runs several dependent ops in one host call
+        o, p = _pair(7, dict(k1=4, m1=1, k2=4, m2=1))
+        from oracle import ec_ref as E
+        B = 2048
+        data = E.blocks(16, B, 5)
+        coding = E.zeros(9, B)
+        o.encode(data, coding, B)
+        D = [x.copy() for x in data]
+        C = [x.copy() for x in coding]
+        for bid in (0, 1, 5):
+            (D[bid] if bid < 16 else C[bid - 16])[:] = 0
+        er = [0, 1, 5, -1]
+        assert p.decode(D, C, B, er, 3) == 0
+        assert same(D, data) and same(C, coding)
+    finally:
+        ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, saved)
+
+
 def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
     """Every ECG_OPT_* setting (grid map incl. auto, NT policy, chunk size) gives identical bytes, for an
     in-stripe encode, a separate-buffer decode and S values that do / do not divide by 8."""
@@ -519,7 +559,7 @@ def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
     k, m, B = 10, 4, 3 * 8192 + 16
     n = k + m
     M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
-    saved = [ecg.get_option(o) for o in range(3)]
+    saved = [ecg.get_option(o) for o in range(ecg.ECG_OPT_COUNT)]
     try:
         for S in (16, 13):
             stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
