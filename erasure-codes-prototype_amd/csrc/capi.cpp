@@ -2,6 +2,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/ecg.h"
@@ -116,6 +117,34 @@ int ecg_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptr
     for (int i = 0; i < k; i++) blocks[i] = (uint8_t*)data_ptrs[i];
     for (int i = 0; i < m; i++) blocks[(size_t)k + i] = (uint8_t*)coding_ptrs[i];
     return Engine::instance().run_host({op}, blocks.data(), k + m, size);
+}
+
+int ecg_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id, char** data_ptrs,
+                                char** coding_ptrs, int size) {
+    if (w != 8 || k < 1 || !matrix_row || dest_id < 0 || size < 0) return ECG_EINVAL;
+    int max_id = dest_id;
+    LinearOp op;
+    for (int i = 0; i < k; i++) {
+        const int c = matrix_row[i];
+        if (c < 0 || c > 255) return ECG_EINVAL;
+        const int id = src_ids ? src_ids[i] : i;
+        if (id < 0) return ECG_EINVAL;
+        if (c == 0) continue;
+        op.src_ids.push_back(id);
+        op.coef.push_back((uint8_t)c);
+        max_id = std::max(max_id, id);
+    }
+    if (op.src_ids.empty()) return ECG_OK;  // all-zero row: destination untouched
+    // dest among its own sources: Jerasure's in-place sequential update would depend on term order;
+    // the reference never asks for it (destinations are coding or erased blocks), so refuse it
+    if (std::find(op.src_ids.begin(), op.src_ids.end(), dest_id) != op.src_ids.end()) return ECG_EINVAL;
+    op.dst_ids.push_back(dest_id);
+    std::vector<uint8_t*> blocks((size_t)max_id + 1, nullptr);
+    for (int id = 0; id <= max_id; id++) {
+        char** base = id < k ? data_ptrs : coding_ptrs;
+        blocks[id] = base ? (uint8_t*)base[id < k ? id : id - k] : nullptr;
+    }
+    return Engine::instance().run_host({op}, blocks.data(), max_id + 1, size);
 }
 
 int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,

@@ -61,7 +61,7 @@ EXPORTS = [
     "ecg_reed_sol_vandermonde_coding_matrix", "ecg_cauchy_good_general_coding_matrix",
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
     "ecg_jerasure_invert_matrix", "ecg_jerasure_matrix_multiply", "ecg_galois_region_xor",
-    "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode",
+    "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode", "ecg_jerasure_matrix_dotprod",
     "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
     "ecg_encode_batch",
     "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
@@ -155,6 +155,7 @@ def lib():
         "ecg_galois_region_xor": ([P, P, I], I),
         "ecg_jerasure_matrix_encode": ([I, I, I, IP, PP, PP, I], I),
         "ecg_jerasure_matrix_decode": ([I, I, I, IP, I, IP, PP, PP, I], I),
+        "ecg_jerasure_matrix_dotprod": ([I, I, IP, IP, I, PP, PP, I], I),
         "ecg_dev_matrix_encode": ([I, I, IP, PP, PP, LL, P], I),
         "ecg_dev_matrix_decode": ([I, I, IP, I, IP, PP, PP, LL, P], I),
         "ecg_matrix_apply_batch": ([I, I, IP, IP, IP, P, LL, LL, P, LL, LL, LL, I, P], I),
@@ -294,6 +295,13 @@ def galois_region_xor(src, dst, n):
 def jerasure_matrix_encode(k, m, matrix, data, coding, size, w=8):
     return _check(lib().ecg_jerasure_matrix_encode(k, m, w, _ints(matrix), _ptrs(data), _ptrs(coding), size),
                   "jerasure_matrix_encode")
+
+
+def jerasure_matrix_dotprod(k, matrix_row, src_ids, dest_id, data, coding, size, w=8):
+    """jerasure_matrix_dotprod (host buffers): one coefficient row into block dest_id."""
+    return _check(lib().ecg_jerasure_matrix_dotprod(k, w, _ints(matrix_row), _ints(src_ids) if src_ids else None,
+                                                     dest_id, _ptrs(data) if data else None,
+                                                     _ptrs(coding) if coding else None, size), "jerasure_matrix_dotprod")
 
 
 def jerasure_matrix_decode(k, m, matrix, row_k_ones, erasures, data, coding, size, w=8):

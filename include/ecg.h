@@ -72,6 +72,12 @@ int* ecg_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int 
 int ecg_galois_region_xor(char* src, char* dest, int nbytes);
 /* Replaces jerasure_matrix_encode              (called rs.cpp:24; lrc.cpp:28; erasure_code.cpp:90,109,147) */
 int ecg_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs, int size);
+/* jerasure_matrix_dotprod (internal to a1/a3 in the reference): one row of k
+ * coefficients into block dest_id (< k: data_ptrs[dest_id], else coding_ptrs[dest_id - k]); sources
+ * are data_ptrs[0..k-1], or src_ids[i] in the same numbering.  An all-zero row leaves dest untouched.
+ * ECG_EINVAL if dest is one of its own (nonzero-coefficient) sources. */
+int ecg_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id, char** data_ptrs,
+                                char** coding_ptrs, int size);
 /* Replaces jerasure_matrix_decode              (called rs.cpp:36; lrc.cpp:50,66).  0 or -1 like the library. */
 int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
                                char** coding_ptrs, int size);

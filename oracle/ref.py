@@ -55,6 +55,7 @@ def lib():
         L.orc_region_xor.argtypes = [P, P, Lg]
         L.orc_region_multiply.argtypes = [P, I, Lg, P, I]
         L.orc_matrix_encode.argtypes = [I, I, IP, PP, PP, Lg]
+        L.orc_matrix_dotprod.argtypes = [I, IP, IP, I, PP, PP, Lg]
         L.orc_matrix_encode_simd.argtypes = [I, I, IP, PP, PP, Lg]
         L.orc_matrix_decode.argtypes = [I, I, IP, I, IP, PP, PP, Lg]
         L.orc_encode_batch_mt.argtypes = [I, I, IP, P, P, Lg, Lg, I]
@@ -132,6 +133,11 @@ def jerasure_matrix_encode(k, m, matrix, data, coding, size):
 
 def jerasure_matrix_encode_simd(k, m, matrix, data, coding, size):
     lib().orc_matrix_encode_simd(k, m, _ints(matrix), _ptrs(data), _ptrs(coding), size)
+
+
+def jerasure_matrix_dotprod(k, row, src_ids, dest_id, data, coding, size):
+    lib().orc_matrix_dotprod(k, _ints(row), _ints(src_ids) if src_ids else None, dest_id,
+                             _ptrs(data) if data else None, _ptrs(coding) if coding else None, size)
 
 
 def jerasure_matrix_decode(k, m, matrix, row_k_ones, erasures, data, coding, size) -> int:

@@ -107,6 +107,33 @@ def test_matrix_decode_quirky_matrices(ecg, oracle, torch_cuda):
         assert ra == rb and same(A, Bb), (k, m, M, pat, rko)
 
 
+def test_matrix_dotprod(ecg, oracle, torch_cuda):
+    """jerasure_matrix_dotprod (row a2): data sources or src_ids mixing data and coding blocks, any
+    destination, coefficient 0/1/other; an all-zero row leaves the destination untouched."""
+    rng = random.Random(11)
+    for trial in range(40):
+        k, m, B = rng.randint(1, 12), rng.randint(1, 5), rng.choice([1, 17, 1024, 4099])
+        row = [rng.choice([0, 1, rng.randrange(256)]) for _ in range(k)]
+        if trial % 7 == 0:
+            row = [0] * k
+        src = None if trial % 2 else [rng.randrange(k + m) for _ in range(k)]
+        dest = rng.randrange(k + m)
+        eff = [(src[i] if src else i) for i in range(k) if row[i]]
+        if dest in eff:  # aliasing is refused (ECG_EINVAL), never computed
+            data = [rnd(B, j) for j in range(k)]
+            coding = [rnd(B, 99 + j) for j in range(m)]
+            with pytest.raises(ecg.EcgError):
+                ecg.jerasure_matrix_dotprod(k, row, src, dest, data, coding, B)
+            continue
+        data = [rnd(B, trial * 31 + j) for j in range(k)]
+        coding = [rnd(B, 500 + trial * 31 + j) for j in range(m)]
+        a = [x.copy() for x in data], [x.copy() for x in coding]
+        b = [x.copy() for x in data], [x.copy() for x in coding]
+        oracle.jerasure_matrix_dotprod(k, row, src, dest, a[0], a[1], B)
+        ecg.jerasure_matrix_dotprod(k, row, src, dest, b[0], b[1], B)
+        assert same(a[0] + a[1], b[0] + b[1]), (trial, k, row, src, dest)
+
+
 def test_galois_region_xor(ecg, oracle, torch_cuda):
     for n in (1, 17, 4096, 100003):
         s, d = rnd(n, 1), rnd(n, 2)
