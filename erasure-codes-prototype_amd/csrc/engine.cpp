@@ -368,7 +368,9 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
                         const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
                         long long out_sstride, long long out_bstride, long long B, hipStream_t st,
                         const int* d_stripe_of) {
-    if (S < 1 || B < 0 || !in_base || !out_base) return ECG_EINVAL;
+    if (S < 0 || B < 0) return ECG_EINVAL;
+    if (S == 0 || B == 0) return ECG_OK;  // empty batch: nothing to read or write
+    if (!in_base || !out_base) return ECG_EINVAL;
     if (progs.size() > 1 && !d_prog_of_stripe) return ECG_EINVAL;
     int status = ECG_OK;
     std::shared_ptr<ProgramSet> ps = program_set(progs, &status);
@@ -401,7 +403,9 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
 
 int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
                      bool aligned, hipStream_t st) {
-    if (S < 1 || B < 0 || !d_src || !d_dst) return ECG_EINVAL;
+    if (S < 0 || B < 0) return ECG_EINVAL;
+    if (S == 0 || B == 0) return ECG_OK;
+    if (!d_src || !d_dst) return ECG_EINVAL;
     int status = ECG_OK;
     std::shared_ptr<ProgramSet> ps = program_set({prog}, &status);
     if (!ps) return status;
@@ -426,7 +430,9 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
 int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long in_sstride, long long in_bstride,
                               void* h_out, long long out_sstride, long long out_bstride, long long B, int S,
                               int chunk) {
-    if (S < 1 || B < 1 || !h_in || !h_out || prog.k_in() < 1 || prog.m_out() < 1) return ECG_EINVAL;
+    if (S < 0 || B < 0 || prog.k_in() < 1 || prog.m_out() < 1) return ECG_EINVAL;
+    if (S == 0 || B == 0) return ECG_OK;
+    if (!h_in || !h_out) return ECG_EINVAL;
     if (chunk < 1) chunk = 16;
     if (chunk > S) chunk = S;
     const int kin = prog.k_in(), mout = prog.m_out();

@@ -85,7 +85,8 @@ int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones,
 /* ---------------------------------------------------------------- tier 2: device / batched
  * All pointers below are DEVICE pointers; `stream` is a hipStream_t (NULL = default stream);
  * calls are asynchronous.  Block pointers must be 16-byte aligned for the vector path (otherwise a
- * byte path runs).  B is any byte count. */
+ * byte path runs).  B is any byte count.  An empty batch (S == 0 or B == 0) is a no-op returning 0;
+ * negative S or B is ECG_EINVAL. */
 int ecg_dev_matrix_encode(int k, int m, const int* matrix, char** d_data_ptrs, char** d_coding_ptrs, long long B,
                           void* stream);
 int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const int* erasures, char** d_data_ptrs,

@@ -171,6 +171,8 @@ static int *big_vandermonde_distribution(int rows, int cols)
 /* reed_sol_vandermonde_coding_matrix(k, m, 8): rows k..k+m-1 of the distribution matrix. */
 int *orc_reed_sol_vandermonde_coding_matrix(int k, int m)
 {
+    /* k < 1 or m < 1: the library's loops are ill-defined there; the oracle declines like the product */
+    if (k < 1 || m < 1) return NULL;
     int *d = big_vandermonde_distribution(k + m, k);
     if (!d) return NULL;
     int *out = (int *)malloc((size_t)m * k * sizeof(int));

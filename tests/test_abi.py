@@ -36,12 +36,21 @@ def test_no_oracle_in_product():
     assert "oracle" not in deps
 
 
-@pytest.mark.parametrize("k,m", [(1, 1), (6, 2), (6, 4), (10, 4), (12, 4), (8, 1), (20, 4), (24, 8), (100, 4)])
+@pytest.mark.parametrize("k,m", [(1, 1), (6, 2), (6, 4), (10, 4), (12, 4), (8, 1), (20, 4), (24, 8), (100, 4),
+                                 (250, 6), (200, 56), (128, 128), (255, 1), (1, 255)])
 def test_vandermonde_parity(ecg, oracle, k, m):
     assert ecg.reed_sol_vandermonde_coding_matrix(k, m) == oracle.reed_sol_vandermonde_coding_matrix(k, m)
 
 
-@pytest.mark.parametrize("k,m", [(8, 3), (12, 3), (10, 4), (5, 5), (20, 6), (8, 2)])
+@pytest.mark.parametrize("k,m", [(256, 1), (1, 256), (200, 57), (0, 4), (4, 0)])
+def test_vandermonde_field_limit(ecg, oracle, k, m):
+    """k + m > 2^w has no Vandermonde code: NULL from both, like the library (reed_sol.c's
+    big_vandermonde_distribution_matrix refuses rows > 2^w).  An empty side is refused too."""
+    assert ecg.reed_sol_vandermonde_coding_matrix(k, m) is None
+    assert oracle.reed_sol_vandermonde_coding_matrix(k, m) is None
+
+
+@pytest.mark.parametrize("k,m", [(8, 3), (12, 3), (10, 4), (5, 5), (20, 6), (8, 2), (200, 56), (100, 4), (3, 253)])
 def test_cauchy_parity(ecg, oracle, k, m):
     assert ecg.cauchy_good_general_coding_matrix(k, m) == oracle.cauchy_good_general_coding_matrix(k, m)
     assert ecg.cauchy_original_coding_matrix(k, m) == oracle.cauchy_original_coding_matrix(k, m)

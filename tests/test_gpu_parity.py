@@ -616,3 +616,93 @@ def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
     finally:
         for o, v in enumerate(saved):
             ecg.set_option(o, v)
+
+
+# ------------------------------------------------------------------ edge sizes: the GF(2^8) field limit, empty inputs
+
+@pytest.mark.parametrize("k,m", [(250, 6), (200, 56), (128, 128), (255, 1), (1, 255)])
+def test_max_field_rs_encode_decode(ecg, oracle, torch_cuda, k, m):
+    """k + m = 256, the largest stripe reed_sol_vandermonde_coding_matrix allows at w = 8: pointer-table
+    launches (k > 128 inputs or m > 32 outputs), up to 32 row tiles, decode with exactly m erasures
+    (a k x k inverse of up to 255 x 255 on the host), B with a byte tail."""
+    torch = torch_cuda
+    B = 4099
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    assert ecg.reed_sol_vandermonde_coding_matrix(k, m) == M
+    assert ecg.reed_sol_vandermonde_coding_matrix(k, m + 1) is None  # k + m + 1 = 257 > 2^w
+    data = [rnd(B, 7 * j + k) for j in range(k)]
+    a = [np.zeros(B, np.uint8) for _ in range(m)]
+    b = [np.full(B, 0xA5, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, data, a, B)
+    ecg.jerasure_matrix_encode(k, m, M, data, b, B)
+    assert same(a, b)
+    stripe = data + a
+    rng = random.Random(k * 1000 + m)
+    for pat in (rng.sample(range(k + m), m), list(range(k + m - m, k + m)), rng.sample(range(k + m), max(1, m // 2))):
+        A = [x.copy() for x in stripe]
+        Bb = [x.copy() for x in stripe]
+        for i in pat:
+            A[i][:] = 0xEE
+            Bb[i][:] = 0xEE
+        ra = oracle.jerasure_matrix_decode(k, m, M, 1, pat + [-1], A[:k], A[k:], B)
+        rb = ecg.jerasure_matrix_decode(k, m, M, 1, pat + [-1], Bb[:k], Bb[k:], B)
+        assert ra == rb == 0, pat
+        assert same(A, Bb) and same(A, stripe), pat
+    # m + 1 erasures: undecodable, -1 like the library, buffers untouched
+    pat = rng.sample(range(k + m), min(k + m, m + 1))
+    if len(pat) == m + 1:
+        A = [x.copy() for x in stripe]
+        assert ecg.jerasure_matrix_decode(k, m, M, 1, pat + [-1], A[:k], A[k:], B) == -1
+        assert same(A, stripe)
+    # batched device tier at the same size: [S][k+m][B'] with B' = 4 KiB + 16
+    S, Bd = 3, 4096 + 16
+    st = torch.empty((S, k + m, Bd), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, 0xF1E1D + k)
+    ecg.encode_batch(k, m, M, st[:, :k], st[:, k:])
+    host = st.cpu().numpy()
+    for s in range(S):
+        ref_c = [np.zeros(Bd, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode(k, m, M, [host[s, j] for j in range(k)], ref_c, Bd)
+        assert all(np.array_equal(ref_c[i], host[s, k + i]) for i in range(m)), s
+
+
+@pytest.mark.parametrize("k,m", [(200, 56), (100, 4)])
+def test_max_field_cauchy_good(ecg, oracle, torch_cuda, k, m):
+    B = 1000
+    C = oracle.cauchy_good_general_coding_matrix(k, m)
+    assert ecg.cauchy_good_general_coding_matrix(k, m) == C
+    data = [rnd(B, 3 * j + m) for j in range(k)]
+    a = [np.zeros(B, np.uint8) for _ in range(m)]
+    b = [np.zeros(B, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, C, data, a, B)
+    ecg.jerasure_matrix_encode(k, m, C, data, b, B)
+    assert same(a, b)
+
+
+def test_empty_inputs(ecg, oracle, torch_cuda):
+    """B = 0 and S = 0 are no-ops that return 0 and touch nothing; negative sizes are ECG_EINVAL."""
+    torch = torch_cuda
+    k, m = 10, 4
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    e0 = np.zeros(0, np.uint8)
+    ecg.jerasure_matrix_encode(k, m, M, [e0] * k, [e0.copy() for _ in range(m)], 0)
+    assert ecg.jerasure_matrix_decode(k, m, M, 1, [0, -1], [e0] * k, [e0.copy() for _ in range(m)], 0) == 0
+    guard = torch.full((2, k + m, 64), 7, dtype=torch.uint8, device="cuda")
+    ecg.encode_batch(k, m, M, guard[:0, :k], guard[:0, k:])                        # S = 0
+    ecg.encode_batch(k, m, M, guard[:, :k, :0], guard[:, k:, :0])                   # B = 0
+    ecg.decode_batch(k, m, M, 1, [[3]], guard[:0])
+    ecg.perform_addition_batch(2, 1, guard[:0, :2], guard[:0, 2:3])
+    ecg.matrix_apply_batch([[1, 1]], [0, 1], [0], guard[:0, :2], guard[:0, 2:3])
+    h = np.zeros((0, k + m, 64), np.uint8)
+    ecg.encode_batch_host(k, m, M, h[:, :k], h[:, k:])
+    torch.cuda.synchronize()
+    assert bool((guard == 7).all())
+    L = ecg.lib()
+    rc = L.ecg_encode_batch(k, m, ecg._ints(M), guard.data_ptr(), guard.stride(0), guard.stride(1),
+                            guard.data_ptr() + k * 64, guard.stride(0), guard.stride(1), 64, -1, None)
+    assert rc == ecg.ECG_EINVAL
+    rc = L.ecg_encode_batch(k, m, ecg._ints(M), guard.data_ptr(), guard.stride(0), guard.stride(1),
+                            guard.data_ptr() + k * 64, guard.stride(0), guard.stride(1), -5, 2, None)
+    assert rc == ecg.ECG_EINVAL
+    torch.cuda.synchronize()
+    assert bool((guard == 7).all())

@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU parity suite only.
+# GPU parity suite only (one process; per-test timeout interrupts a test stuck in a GPU call).
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600 "$@" > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread "$@" > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
-echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/pytest_gpu.log | tail -30
+echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed|Timeout" gpurun_out/pytest_gpu.log | tail -30
 exit $rc
