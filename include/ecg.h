@@ -7,7 +7,7 @@
  *     "Jerasure gf_complete"), same arguments and semantics, w = 8 only.  Region arguments are HOST
  *     pointers (char** of B-byte buffers, as the proxy passes them: proxy.cpp:335-346); the bytes are
  *     staged through HBM and computed by the HIP kernels.  The reference's src/ec/{rs,lrc,pc,erasure_code}.cpp can be
- *     relinked against these symbols unchanged (INTEGRATION.md shows the shim header).
+ *     relinked against these symbols unchanged through the shim headers in include/jerasure_shim/.
  *  2. Device / batched tier — the same operations over HBM-resident blocks, asynchronous on a HIP
  *     stream, and batches of S stripes in one launch (what bench.py drives).
  *  3. ErasureCode facade — handles mirroring the reference's ErasureCode class hierarchy
