@@ -385,6 +385,20 @@ int ecg_ec_encode_partial_blocks_for_decoding(ecg_ec* ec, char** data_ptrs, char
                                                         vec(failure_idxs, n_failures));
 }
 
+int ecg_ec_encode_partial_blocks_for_decoding_with_addition(ecg_ec* ec, char** local_ptrs, char** partial_ptrs,
+                                                            int n_partials, char** out_ptrs, int block_size,
+                                                            const int* local_survivor_idxs, int n_local,
+                                                            const int* survivor_idxs, int n_survivors,
+                                                            const int* failure_idxs, int n_failures) {
+    if (!ec || !out_ptrs || n_local < 0 || n_partials < 0 || n_failures < 1 || block_size < 0) return ECG_EINVAL;
+    if ((n_local > 0 && (!local_ptrs || !local_survivor_idxs || !survivor_idxs || n_survivors < 1)) ||
+        (n_partials > 0 && !partial_ptrs) || !failure_idxs)
+        return ECG_EINVAL;
+    return ec->impl->encode_partial_blocks_for_decoding_with_addition(
+        local_ptrs, partial_ptrs, n_partials, out_ptrs, block_size, vec(local_survivor_idxs, n_local),
+        vec(survivor_idxs, n_survivors), vec(failure_idxs, n_failures));
+}
+
 int ecg_ec_perform_addition(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size, int block_num,
                             int parity_num) {
     if (!ec || block_size < 0) return ECG_EINVAL;

@@ -69,6 +69,15 @@ public:
                                            std::vector<int> local_survivor_idxs, std::vector<int> survivor_idxs,
                                            std::vector<int> failure_idxs);
     int perform_addition(char** data_ptrs, char** coding_ptrs, int block_size, int block_num, int parity_num);
+    // The main proxy's two steps of a partial-decoding repair (handle_repair.cpp:371-376) in one pass:
+    // out[u] = (encode_partial_blocks_for_decoding over local_ptrs)[u] XOR perform_addition over
+    // partial_ptrs (n_partials = cnt * f, interleaved like perform_addition's input).  Reads each local
+    // block and each helper partial once and writes the f outputs once (the separate calls also write
+    // and re-read the main proxy's own f partials).  local_survivor_idxs may be empty.
+    int encode_partial_blocks_for_decoding_with_addition(char** local_ptrs, char** partial_ptrs, int n_partials,
+                                                         char** out_ptrs, int block_size,
+                                                         std::vector<int> local_survivor_idxs,
+                                                         std::vector<int> survivor_idxs, std::vector<int> failure_idxs);
 
     // The coefficient matrix (n_out x n_in) a partial call applies (erasure_code.cpp:97-150 semantics).
     virtual int partial_encoding_matrix(std::vector<int> data_idxs, std::vector<int> parity_idxs,

@@ -70,7 +70,8 @@ EXPORTS = [
     "ecg_ec_set_memory", "ecg_ec_set_isvertical", "ecg_ec_k", "ecg_ec_m", "ecg_ec_make_encoding_matrix",
     "ecg_ec_check_if_decodable", "ecg_ec_encode", "ecg_ec_decode",
     "ecg_ec_encode_partial_blocks_for_encoding", "ecg_ec_encode_partial_blocks_for_decoding",
-    "ecg_ec_perform_addition", "ecg_ec_partial_decoding_matrix", "ecg_ec_partial_encoding_matrix",
+    "ecg_ec_perform_addition", "ecg_ec_encode_partial_blocks_for_decoding_with_addition",
+    "ecg_ec_partial_decoding_matrix", "ecg_ec_partial_encoding_matrix",
     "ecg_ec_set_placement_rule", "ecg_ec_set_random_seed", "ecg_ec_generate_partition", "ecg_ec_get_partition",
     "ecg_ec_set_partition", "ecg_ec_grouping_information", "ecg_ec_generate_repair_plan", "ecg_ec_self_information",
     "ecg_ec_bid2gid", "ecg_ec_idxingroup", "ecg_ec_get_group_size", "ecg_ec_bid2rowcol", "ecg_ec_rowcol2bid",
@@ -181,6 +182,7 @@ def lib():
         "ecg_ec_encode_partial_blocks_for_encoding": ([P, PP, PP, I, IP, I, IP, I], I),
         "ecg_ec_encode_partial_blocks_for_decoding": ([P, PP, PP, I, IP, I, IP, I, IP, I], I),
         "ecg_ec_perform_addition": ([P, PP, PP, I, I, I], I),
+        "ecg_ec_encode_partial_blocks_for_decoding_with_addition": ([P, PP, PP, I, PP, I, IP, I, IP, I, IP, I], I),
         "ecg_ec_partial_decoding_matrix": ([P, IP, I, IP, I, IP, I, IP, I], I),
         "ecg_ec_partial_encoding_matrix": ([P, IP, I, IP, I, IP, I], I),
         "ecg_ec_set_placement_rule": ([P, I], I),
@@ -509,6 +511,17 @@ class ErasureCode:
         self._bind(list(data_ptrs) + list(coding_ptrs), stream)
         return lib().ecg_ec_perform_addition(self._h, _ptrs(data_ptrs), _ptrs(coding_ptrs), block_size, block_num,
                                              parity_num)
+
+    def encode_partial_blocks_for_decoding_with_addition(self, local_ptrs, partial_ptrs, out_ptrs, block_size,
+                                                         local_survivor_idxs, survivor_idxs, failure_idxs,
+                                                         stream=None):
+        """The main proxy's own partial + perform_addition of the helpers' partials in one pass
+        (handle_repair.cpp:371-376)."""
+        self._bind(list(local_ptrs) + list(partial_ptrs) + list(out_ptrs), stream)
+        return _check(lib().ecg_ec_encode_partial_blocks_for_decoding_with_addition(
+            self._h, _ptrs(local_ptrs), _ptrs(partial_ptrs), len(partial_ptrs), _ptrs(out_ptrs), block_size,
+            _ints(local_survivor_idxs), len(local_survivor_idxs), _ints(survivor_idxs), len(survivor_idxs),
+            _ints(failure_idxs), len(failure_idxs)), "encode_partial_blocks_for_decoding_with_addition")
 
     # --- planning hooks (batched repair / merge)
     def partial_decoding_matrix(self, local_survivor_idxs, survivor_idxs, failure_idxs):

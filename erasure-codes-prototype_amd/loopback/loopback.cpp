@@ -213,21 +213,24 @@ struct Loopback::Impl {
         out.assign(f, Block(B, 0));
         last_kind = std::string(partial ? "partial-" : "direct-") + (p.cp.local_or_column ? "local" : "global");
         if (partial) {
-            if (!orig.empty()) {  // the main cluster's own partial
-                std::vector<Block> own(f, Block(B));
-                auto dp = ptrs(orig), op = ptrs(own);
+            // The main cluster's own partial over its blocks, then perform_addition with the helpers'
+            // partials (handle_repair.cpp:371-376), done as ONE call: the own partial never round-trips.
+            auto op = ptrs(out);
+            if (partials.empty()) {
+                if (orig.empty()) return false;
+                auto dp = ptrs(orig);
                 if (!ok(ecg_ec_encode_partial_blocks_for_decoding(ec.h, dp.data(), op.data(), (int)B, orig_idx.data(),
                                                                   (int)orig_idx.size(), p.live.data(),
                                                                   (int)p.live.size(), p.failed.data(), f)))
                     return false;
-                for (auto& b : own) partials.push_back(std::move(b));
-            }
-            const int data_num = (int)partials.size();
-            if (data_num == f) {
+            } else if (orig.empty() && (int)partials.size() == f) {
                 out = partials;
             } else {
-                auto dp = ptrs(partials), op = ptrs(out);
-                if (!ok(ecg_ec_perform_addition(ec.h, dp.data(), op.data(), (int)B, data_num, f))) return false;
+                auto dp = ptrs(orig), pp = ptrs(partials);
+                if (!ok(ecg_ec_encode_partial_blocks_for_decoding_with_addition(
+                        ec.h, dp.data(), pp.data(), (int)partials.size(), op.data(), (int)B, orig_idx.data(),
+                        (int)orig_idx.size(), p.live.data(), (int)p.live.size(), p.failed.data(), f)))
+                    return false;
             }
             L.stats.plans_partial++;
             return true;

@@ -180,6 +180,16 @@ int ecg_ec_encode_partial_blocks_for_decoding(ecg_ec* ec, char** data_ptrs, char
                                               const int* failure_idxs, int n_failures);
 int ecg_ec_perform_addition(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size, int block_num,
                             int parity_num);
+/* The main proxy's end of a partial-decoding repair (handle_repair.cpp:371-376: its own
+ * encode_partial_blocks_for_decoding over local_ptrs, then perform_addition with the helpers' partials)
+ * in ONE pass: out[u] = partial_u(local blocks) XOR (XOR_j partial_ptrs[j*n_failures + u]).  Same bytes
+ * as the two calls, without writing and re-reading the main proxy's own partials.  n_local may be 0
+ * (pure addition); n_partials must be a multiple of n_failures. */
+int ecg_ec_encode_partial_blocks_for_decoding_with_addition(ecg_ec* ec, char** local_ptrs, char** partial_ptrs,
+                                                            int n_partials, char** out_ptrs, int block_size,
+                                                            const int* local_survivor_idxs, int n_local,
+                                                            const int* survivor_idxs, int n_survivors,
+                                                            const int* failure_idxs, int n_failures);
 /* Planning hooks for batching: the coefficient matrix (n_out x n_in, row-major) that the facade's
  * partial call would apply to its data_ptrs -> coding_ptrs.  Returns n_out (>= 0) or a negative code;
  * feed the result to ecg_matrix_apply_batch. */

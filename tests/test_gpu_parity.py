@@ -254,6 +254,75 @@ def test_facade_partials_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
             assert same(da, db), ("dec", local, lsub, surv, lost)
 
 
+@pytest.mark.parametrize("t,params,local", [(0, dict(k=10, m=4), False), (0, dict(k=6, m=4), False),
+                                             (2, dict(k=12, l=2, g=2), True), (2, dict(k=12, l=2, g=2), False)])
+def test_main_repair_with_addition(ecg, oracle, torch_cuda, t, params, local):
+    """encode_partial_blocks_for_decoding_with_addition == the main proxy's own partial followed by
+    perform_addition over [helper partials..., own partials] (handle_repair.cpp:371-376), and == the lost
+    blocks; also with no local blocks (pure addition) and no helper partials (own partial only)."""
+    from oracle import ec_ref as E
+    rng = random.Random(t * 10 + params["k"] + local)
+    B = 4096 + 3
+    o, p = _pair(t, params, local)
+    data = E.blocks(o.k, B, 5)
+    coding = E.zeros(o.m, B)
+    o.encode(data, coding, B)
+    stripe = data + coding
+    for trial in range(8):
+        if local:
+            gid = rng.randrange(o.l)
+            gs, mn = o.get_group_size(gid)
+            group = list(range(mn, mn + gs)) + [o.k + o.g + gid]
+            f = 1
+        else:
+            group = list(range(o.k)) + list(range(o.k, o.k + (o.g if hasattr(o, "g") else o.m)))
+            f = rng.randint(1, min(3, len(group) - o.k))
+        lost = rng.sample(group, f)
+        need = len(group) - 1 if local else o.k  # encode_partial_blocks_for_decoding takes exactly k' survivors
+        surv = [i for i in group if i not in lost][:need]
+        parts = [[], [], []]
+        for i in surv:
+            parts[rng.randrange(3)].append(i)
+        if trial == 0:
+            parts = [surv[:len(surv) // 2], surv[len(surv) // 2:], []]  # main holds no block
+        if trial == 1:
+            parts = [[], [], surv]                                        # no helper partials
+        helper_partials = []
+        for h in parts[:2]:
+            if h:
+                out = E.zeros(f, B)
+                o.encode_partial_blocks_for_decoding([stripe[i] for i in h], out, B, h, surv, lost)
+                helper_partials += out
+        mine = parts[2]
+        expect = E.zeros(f, B)
+        if mine:
+            own = E.zeros(f, B)
+            o.encode_partial_blocks_for_decoding([stripe[i] for i in mine], own, B, mine, surv, lost)
+        else:
+            own = []
+        allp = helper_partials + own
+        if len(allp) == f:
+            expect = allp
+        else:
+            o.perform_addition(allp, expect, B, len(allp), f)
+        got = [np.full(B, 0x77, np.uint8) for _ in range(f)]
+        assert p.encode_partial_blocks_for_decoding_with_addition(
+            [stripe[i] for i in mine], helper_partials, got, B, mine, surv, lost) == 0
+        assert same(got, expect), (trial, parts, lost)
+        assert same(got, [stripe[i] for i in lost]), (trial, parts, lost)
+    # device tier, same call on HBM buffers
+    torch = torch_cuda
+    mine, hp_host = surv[:2], E.zeros(f, B)
+    rest = surv[2:]
+    o.encode_partial_blocks_for_decoding([stripe[i] for i in rest], hp_host, B, rest, surv, lost)
+    d_loc = [torch.from_numpy(stripe[i]).cuda() for i in mine]
+    d_hp = [torch.from_numpy(x).cuda() for x in hp_host]
+    d_out = [torch.zeros(B, dtype=torch.uint8, device="cuda") for _ in range(f)]
+    assert p.encode_partial_blocks_for_decoding_with_addition(d_loc, d_hp, d_out, B, mine, surv, lost) == 0
+    torch.cuda.synchronize()
+    assert same([x.cpu().numpy() for x in d_out], [stripe[i] for i in lost])
+
+
 def test_perform_addition(ecg, oracle, torch_cuda):
     from oracle import ec_ref as E
     o = E.RSCode(4, 2)
