@@ -399,6 +399,18 @@ int ecg_ec_encode_partial_blocks_for_decoding_with_addition(ecg_ec* ec, char** l
         vec(survivor_idxs, n_survivors), vec(failure_idxs, n_failures));
 }
 
+int ecg_ec_encode_partial_blocks_for_encoding_with_addition(ecg_ec* ec, char** local_ptrs, char** partial_ptrs,
+                                                            int n_partials, char** out_ptrs, int block_size,
+                                                            const int* data_idxs, int n_data, const int* parity_idxs,
+                                                            int n_parity) {
+    if (!ec || !out_ptrs || n_data < 0 || n_partials < 0 || n_parity < 1 || !parity_idxs || block_size < 0)
+        return ECG_EINVAL;
+    if ((n_data > 0 && (!local_ptrs || !data_idxs)) || (n_partials > 0 && !partial_ptrs)) return ECG_EINVAL;
+    return ec->impl->encode_partial_blocks_for_encoding_with_addition(local_ptrs, partial_ptrs, n_partials, out_ptrs,
+                                                                      block_size, vec(data_idxs, n_data),
+                                                                      vec(parity_idxs, n_parity));
+}
+
 int ecg_ec_perform_addition(ecg_ec* ec, char** data_ptrs, char** coding_ptrs, int block_size, int block_num,
                             int parity_num) {
     if (!ec || block_size < 0) return ECG_EINVAL;

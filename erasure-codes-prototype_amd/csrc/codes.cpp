@@ -170,6 +170,26 @@ int ErasureCode::perform_addition(char** data_ptrs, char** coding_ptrs, int bloc
     return run(p, data_ptrs, block_num, coding_ptrs, parity_num, block_size);
 }
 
+// out[u] = XOR_i R[u][i] * local[i]  XOR  XOR_j partial[j * nf + u]  (one launch)
+int ErasureCode::run_with_addition(const std::vector<int>& R, int nl, int nf, char** local_ptrs,
+                                   char** partial_ptrs, int n_partials, char** out_ptrs, long long B) {
+    LinearOp op;
+    const int n_in = nl + n_partials;
+    op.src_ids = iota_ids(n_in);
+    op.dst_ids = iota_ids(nf, n_in);
+    op.coef.assign((size_t)nf * n_in, 0);
+    for (int u = 0; u < nf; u++) {
+        for (int i = 0; i < nl; i++) op.coef[(size_t)u * n_in + i] = R[(size_t)u * nl + i] & 0xff;
+        for (int j = 0; j < n_partials / nf; j++) op.coef[(size_t)u * n_in + nl + (size_t)j * nf + u] = 1;
+    }
+    std::vector<char*> in((size_t)n_in);
+    for (int i = 0; i < nl; i++) in[i] = local_ptrs[i];
+    for (int j = 0; j < n_partials; j++) in[(size_t)nl + j] = partial_ptrs[j];
+    Plan p;
+    p.ops.push_back(std::move(op));
+    return run(p, in.data(), n_in, out_ptrs, nf, B);
+}
+
 int ErasureCode::encode_partial_blocks_for_decoding_with_addition(char** local_ptrs, char** partial_ptrs,
                                                                   int n_partials, char** out_ptrs, int block_size,
                                                                   std::vector<int> lsi, std::vector<int> si,
@@ -182,20 +202,22 @@ int ErasureCode::encode_partial_blocks_for_decoding_with_addition(char** local_p
         int rc = partial_decoding_matrix(std::move(lsi), std::move(si), std::move(fi), R);
         if (rc != ECG_OK) return rc;
     }
-    LinearOp op;
-    op.src_ids = iota_ids(nl + n_partials);
-    op.dst_ids = iota_ids(nf, nl + n_partials);
-    op.coef.assign((size_t)nf * (nl + n_partials), 0);
-    for (int u = 0; u < nf; u++) {
-        for (int i = 0; i < nl; i++) op.coef[(size_t)u * (nl + n_partials) + i] = R[(size_t)u * nl + i] & 0xff;
-        for (int j = 0; j < n_partials / nf; j++) op.coef[(size_t)u * (nl + n_partials) + nl + j * nf + u] = 1;
+    return run_with_addition(R, nl, nf, local_ptrs, partial_ptrs, n_partials, out_ptrs, block_size);
+}
+
+int ErasureCode::encode_partial_blocks_for_encoding_with_addition(char** local_ptrs, char** partial_ptrs,
+                                                                  int n_partials, char** out_ptrs, int block_size,
+                                                                  std::vector<int> data_idxs,
+                                                                  std::vector<int> parity_idxs) {
+    const int nl = (int)data_idxs.size(), nf = (int)parity_idxs.size();
+    if (nf < 1 || n_partials < 0 || n_partials % nf != 0 || block_size < 0) return ECG_EINVAL;
+    if (nl + n_partials == 0) return ECG_EINVAL;
+    std::vector<int> R;
+    if (nl > 0) {
+        int rc = partial_encoding_matrix(std::move(data_idxs), std::move(parity_idxs), R);
+        if (rc != ECG_OK) return rc;
     }
-    std::vector<char*> in((size_t)nl + n_partials);
-    for (int i = 0; i < nl; i++) in[i] = local_ptrs[i];
-    for (int j = 0; j < n_partials; j++) in[(size_t)nl + j] = partial_ptrs[j];
-    Plan p;
-    p.ops.push_back(std::move(op));
-    return run(p, in.data(), nl + n_partials, out_ptrs, nf, block_size);
+    return run_with_addition(R, nl, nf, local_ptrs, partial_ptrs, n_partials, out_ptrs, block_size);
 }
 
 static bool ids_in_range(const std::vector<int>& v, int n) {

@@ -78,6 +78,11 @@ public:
                                                          char** out_ptrs, int block_size,
                                                          std::vector<int> local_survivor_idxs,
                                                          std::vector<int> survivor_idxs, std::vector<int> failure_idxs);
+    // The same for stripe merging: the parity proxy's own encode_partial_blocks_for_encoding over its data
+    // blocks plus perform_addition with the helpers' partial parities (handle_merge.cpp:159,319).
+    int encode_partial_blocks_for_encoding_with_addition(char** local_ptrs, char** partial_ptrs, int n_partials,
+                                                         char** out_ptrs, int block_size, std::vector<int> data_idxs,
+                                                         std::vector<int> parity_idxs);
 
     // The coefficient matrix (n_out x n_in) a partial call applies (erasure_code.cpp:97-150 semantics).
     virtual int partial_encoding_matrix(std::vector<int> data_idxs, std::vector<int> parity_idxs,
@@ -128,6 +133,8 @@ protected:
     int run(const Plan& plan, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding, long long B);
     // jerasure_matrix_encode / _decode over this call's pointers
     int run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B);
+    int run_with_addition(const std::vector<int>& R, int nl, int nf, char** local_ptrs, char** partial_ptrs,
+                          int n_partials, char** out_ptrs, long long B);
     int run_decode(int kk, int mm, const int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
                    char** coding_ptrs, long long B);
 };

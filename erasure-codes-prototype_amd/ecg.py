@@ -71,6 +71,7 @@ EXPORTS = [
     "ecg_ec_check_if_decodable", "ecg_ec_encode", "ecg_ec_decode",
     "ecg_ec_encode_partial_blocks_for_encoding", "ecg_ec_encode_partial_blocks_for_decoding",
     "ecg_ec_perform_addition", "ecg_ec_encode_partial_blocks_for_decoding_with_addition",
+    "ecg_ec_encode_partial_blocks_for_encoding_with_addition",
     "ecg_ec_partial_decoding_matrix", "ecg_ec_partial_encoding_matrix",
     "ecg_ec_set_placement_rule", "ecg_ec_set_random_seed", "ecg_ec_generate_partition", "ecg_ec_get_partition",
     "ecg_ec_set_partition", "ecg_ec_grouping_information", "ecg_ec_generate_repair_plan", "ecg_ec_self_information",
@@ -183,6 +184,7 @@ def lib():
         "ecg_ec_encode_partial_blocks_for_decoding": ([P, PP, PP, I, IP, I, IP, I, IP, I], I),
         "ecg_ec_perform_addition": ([P, PP, PP, I, I, I], I),
         "ecg_ec_encode_partial_blocks_for_decoding_with_addition": ([P, PP, PP, I, PP, I, IP, I, IP, I, IP, I], I),
+        "ecg_ec_encode_partial_blocks_for_encoding_with_addition": ([P, PP, PP, I, PP, I, IP, I, IP, I], I),
         "ecg_ec_partial_decoding_matrix": ([P, IP, I, IP, I, IP, I, IP, I], I),
         "ecg_ec_partial_encoding_matrix": ([P, IP, I, IP, I, IP, I], I),
         "ecg_ec_set_placement_rule": ([P, I], I),
@@ -522,6 +524,16 @@ class ErasureCode:
             self._h, _ptrs(local_ptrs), _ptrs(partial_ptrs), len(partial_ptrs), _ptrs(out_ptrs), block_size,
             _ints(local_survivor_idxs), len(local_survivor_idxs), _ints(survivor_idxs), len(survivor_idxs),
             _ints(failure_idxs), len(failure_idxs)), "encode_partial_blocks_for_decoding_with_addition")
+
+    def encode_partial_blocks_for_encoding_with_addition(self, local_ptrs, partial_ptrs, out_ptrs, block_size,
+                                                         data_idxs, parity_idxs, stream=None):
+        """The parity proxy's own partial encoding + perform_addition of the helpers' partials in one
+        pass (handle_merge.cpp:159,319)."""
+        self._bind(list(local_ptrs) + list(partial_ptrs) + list(out_ptrs), stream)
+        return _check(lib().ecg_ec_encode_partial_blocks_for_encoding_with_addition(
+            self._h, _ptrs(local_ptrs), _ptrs(partial_ptrs), len(partial_ptrs), _ptrs(out_ptrs), block_size,
+            _ints(data_idxs), len(data_idxs), _ints(parity_idxs), len(parity_idxs)),
+            "encode_partial_blocks_for_encoding_with_addition")
 
     # --- planning hooks (batched repair / merge)
     def partial_decoding_matrix(self, local_survivor_idxs, survivor_idxs, failure_idxs):

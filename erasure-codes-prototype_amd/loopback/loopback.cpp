@@ -554,17 +554,12 @@ struct Loopback::Impl {
         if (!helpers_ok) return false;
         out.assign(np, Block(B, 0));
         auto op = ptrs(out);
-        if (p.partial_decoding) {
-            if (!orig.empty()) {
-                std::vector<Block> own(np, Block(B));
-                auto dp = ptrs(orig), ownp = ptrs(own);
-                if (!ok(ecg_ec_encode_partial_blocks_for_encoding(ec.h, dp.data(), ownp.data(), (int)B, orig_idx.data(),
-                                                                  (int)orig_idx.size(), p.parity_idx.data(), np)))
-                    return false;
-                for (auto& b : own) partials.push_back(std::move(b));
-            }
-            auto dp = ptrs(partials);
-            return ok(ecg_ec_perform_addition(ec.h, dp.data(), op.data(), (int)B, (int)partials.size(), np));
+        if (p.partial_decoding && !partials.empty()) {
+            // own partial encoding + perform_addition (handle_merge.cpp:159,319) in one call
+            auto dp = ptrs(orig), pp = ptrs(partials);
+            return ok(ecg_ec_encode_partial_blocks_for_encoding_with_addition(
+                ec.h, dp.data(), pp.data(), (int)partials.size(), op.data(), (int)B, orig_idx.data(),
+                (int)orig_idx.size(), p.parity_idx.data(), np));
         }
         auto dp = ptrs(orig);
         return ok(ecg_ec_encode_partial_blocks_for_encoding(ec.h, dp.data(), op.data(), (int)B, orig_idx.data(),

@@ -190,6 +190,13 @@ int ecg_ec_encode_partial_blocks_for_decoding_with_addition(ecg_ec* ec, char** l
                                                             const int* local_survivor_idxs, int n_local,
                                                             const int* survivor_idxs, int n_survivors,
                                                             const int* failure_idxs, int n_failures);
+/* Stripe-merging counterpart (handle_merge.cpp:159,319): the parity proxy's own
+ * encode_partial_blocks_for_encoding over local_ptrs plus perform_addition of the helpers' partial
+ * parities, in one pass.  n_data may be 0; n_partials must be a multiple of n_parity. */
+int ecg_ec_encode_partial_blocks_for_encoding_with_addition(ecg_ec* ec, char** local_ptrs, char** partial_ptrs,
+                                                            int n_partials, char** out_ptrs, int block_size,
+                                                            const int* data_idxs, int n_data, const int* parity_idxs,
+                                                            int n_parity);
 /* Planning hooks for batching: the coefficient matrix (n_out x n_in, row-major) that the facade's
  * partial call would apply to its data_ptrs -> coding_ptrs.  Returns n_out (>= 0) or a negative code;
  * feed the result to ecg_matrix_apply_batch. */

@@ -323,6 +323,49 @@ def test_main_repair_with_addition(ecg, oracle, torch_cuda, t, params, local):
     assert same([x.cpu().numpy() for x in d_out], [stripe[i] for i in lost])
 
 
+@pytest.mark.parametrize("t,params", [(0, dict(k=10, m=4)), (1, dict(k=4, m=2, x=3, seri_num=1)),
+                                      (2, dict(k=12, l=2, g=2))])
+def test_merge_recal_with_addition(ecg, oracle, torch_cuda, t, params):
+    """encode_partial_blocks_for_encoding_with_addition == the parity proxy's own partial encoding
+    followed by perform_addition over [helper partials..., own partials] (handle_merge.cpp:159,319), and
+    == the full parities when the parts cover all data."""
+    from oracle import ec_ref as E
+    rng = random.Random(t * 7 + params["k"])
+    B = 2048 + 9
+    o, p = _pair(t, params)
+    data = E.blocks(o.k, B, 9)
+    coding = E.zeros(o.m, B)
+    o.encode(data, coding, B)
+    stripe = data + coding
+    npar = o.g if hasattr(o, "g") else o.m
+    for trial in range(6):
+        par = sorted(rng.sample(range(o.k, o.k + npar), rng.randint(1, npar)))
+        parts = [[], [], []]
+        for i in range(o.k):
+            parts[rng.randrange(3)].append(i)
+        if trial == 0:
+            parts = [list(range(o.k)), [], []]
+        helper_partials = []
+        for h in parts[:2]:
+            if h:
+                out = E.zeros(len(par), B)
+                o.encode_partial_blocks_for_encoding([stripe[i] for i in h], out, B, h, par)
+                helper_partials += out
+        mine = parts[2]
+        own = []
+        if mine:
+            own = E.zeros(len(par), B)
+            o.encode_partial_blocks_for_encoding([stripe[i] for i in mine], own, B, mine, par)
+        allp = helper_partials + own
+        expect = E.zeros(len(par), B)
+        o.perform_addition(allp, expect, B, len(allp), len(par))
+        got = [np.full(B, 0x11, np.uint8) for _ in par]
+        assert p.encode_partial_blocks_for_encoding_with_addition(
+            [stripe[i] for i in mine], helper_partials, got, B, mine, par) == 0
+        assert same(got, expect), (trial, parts, par)
+        assert same(got, [stripe[i] for i in par]), (trial, parts, par)
+
+
 def test_perform_addition(ecg, oracle, torch_cuda):
     from oracle import ec_ref as E
     o = E.RSCode(4, 2)
