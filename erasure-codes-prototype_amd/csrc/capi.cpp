@@ -56,6 +56,10 @@ int ecg_set_device(int device) { return hipSetDevice(device) == hipSuccess ? ECG
 
 void ecg_free(void* p) { free(p); }
 
+int ecg_batch_begin(void) { return batch_begin(); }
+int ecg_batch_flush(void) { return batch_flush(); }
+int ecg_batch_end(void) { return batch_end(); }
+
 int ecg_set_option(int option, long long value) { return set_option(option, value) == 0 ? ECG_OK : ECG_EINVAL; }
 long long ecg_get_option(int option) { return get_option(option); }
 

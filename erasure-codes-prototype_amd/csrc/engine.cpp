@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <unordered_set>
 
 namespace ecg {
 
@@ -232,6 +233,169 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     return ECG_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Deferred-batch scope (engine.hpp).
+
+namespace {
+
+struct DeferredCall {
+    Engine* eng;
+    hipStream_t st;
+    long long B;
+    std::shared_ptr<const std::vector<LinearOp>> ops;  // shared by consecutive calls with the same plan
+    std::vector<uint8_t*> blocks;                      // the call's block space (device pointers)
+};
+
+struct DeferScope {
+    bool active = false;
+    std::vector<DeferredCall> q;
+};
+
+thread_local DeferScope t_defer;
+constexpr size_t kMaxDeferred = 1 << 16;  // calls recorded before an automatic flush
+
+bool same_ops(const std::vector<LinearOp>& a, const std::vector<LinearOp>& b) {
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.size(); i++)
+        if (a[i].src_ids != b[i].src_ids || a[i].dst_ids != b[i].dst_ids || a[i].coef != b[i].coef) return false;
+    return true;
+}
+
+// Pointer tables for pointer-table launches: per-thread ring of pinned host + device slots, a slot
+// reused only after the launch that read it has completed (its event).
+struct TableSlot {
+    void* host = nullptr;
+    void* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+};
+constexpr int kTableSlots = 4;
+thread_local TableSlot t_tables[kMaxDevices][kTableSlots];
+thread_local int t_table_next[kMaxDevices] = {};
+
+}  // namespace
+
+bool batch_active() { return t_defer.active; }
+
+int batch_begin() {
+    if (t_defer.active) return ECG_EINVAL;  // scopes do not nest
+    t_defer.active = true;
+    t_defer.q.clear();
+    return ECG_OK;
+}
+
+int batch_flush() {
+    DeferScope& d = t_defer;
+    if (d.q.empty()) return ECG_OK;
+    std::vector<DeferredCall> q;
+    q.swap(d.q);
+    int rc = ECG_OK;
+    size_t i = 0;
+    while (i < q.size() && rc == ECG_OK) {
+        // run [i, j): same engine / stream / B / plan, and no block written by one call and touched by another
+        std::unordered_set<const uint8_t*> wr, rd;
+        auto touch = [&](const DeferredCall& c, bool check) {
+            for (const LinearOp& op : *c.ops) {
+                for (int id : op.src_ids) {
+                    if (check && wr.count(c.blocks[id])) return false;
+                }
+                for (int id : op.dst_ids) {
+                    if (check && (wr.count(c.blocks[id]) || rd.count(c.blocks[id]))) return false;
+                }
+            }
+            for (const LinearOp& op : *c.ops) {
+                for (int id : op.src_ids) rd.insert(c.blocks[id]);
+                for (int id : op.dst_ids) wr.insert(c.blocks[id]);
+            }
+            return true;
+        };
+        touch(q[i], false);
+        size_t j = i + 1;
+        while (j < q.size() && q[j].eng == q[i].eng && q[j].st == q[i].st && q[j].B == q[i].B &&
+               (q[j].ops == q[i].ops || same_ops(*q[j].ops, *q[i].ops)) && touch(q[j], true))
+            j++;
+        Engine* eng = q[i].eng;
+        if (j - i == 1) {
+            rc = eng->launch_direct(*q[i].ops, q[i].blocks.data(), q[i].B, q[i].st);
+        } else {
+            std::vector<const uint8_t* const*> calls;
+            calls.reserve(j - i);
+            for (size_t c = i; c < j; c++) calls.push_back(q[c].blocks.data());
+            for (const LinearOp& op : *q[i].ops) {
+                if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
+                    for (size_t c = i; c < j && rc == ECG_OK; c++) rc = eng->launch_direct({op}, q[c].blocks.data(), q[c].B, q[c].st);
+                } else {
+                    rc = eng->run_ptr_batch(op, calls, q[i].B, q[i].st);
+                }
+                if (rc != ECG_OK) break;
+            }
+        }
+        i = j;
+    }
+    return rc;
+}
+
+int batch_end() {
+    if (!t_defer.active) return ECG_EINVAL;
+    const int rc = batch_flush();
+    t_defer.active = false;
+    t_defer.q.clear();
+    return rc;
+}
+
+int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* const*>& calls, long long B,
+                          hipStream_t st) {
+    const int S = (int)calls.size(), k = op.k_in(), m = op.m_out();
+    const size_t n = (size_t)S * (k + m);
+    TableSlot& t = t_tables[device_][t_table_next[device_]];
+    t_table_next[device_] = (t_table_next[device_] + 1) % kTableSlots;
+    if (t.pending) {
+        ECG_HIP(hipEventSynchronize(t.ev));
+        t.pending = false;
+    }
+    if (!t.ev) ECG_HIP(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming));
+    if (t.cap < n * sizeof(void*)) {
+        if (t.host) (void)hipHostFree(t.host);
+        if (t.dev) (void)hipFree(t.dev);
+        t.host = t.dev = nullptr;
+        t.cap = 0;
+        const size_t cap = std::max(n * sizeof(void*), (size_t)64 << 10);
+        ECG_HIP(hipHostMalloc(&t.host, cap, hipHostMallocDefault));
+        ECG_HIP(hipMalloc(&t.dev, cap));
+        t.cap = cap;
+    }
+    const uint8_t** h = (const uint8_t**)t.host;
+    bool aligned = true;
+    for (int s = 0; s < S; s++) {
+        for (int j = 0; j < k; j++) {
+            const uint8_t* p = calls[s][op.src_ids[j]];
+            aligned &= aligned16(p);
+            h[(size_t)s * k + j] = p;
+        }
+        for (int q = 0; q < m; q++) {
+            const uint8_t* p = calls[s][op.dst_ids[q]];
+            aligned &= aligned16(p);
+            h[(size_t)S * k + (size_t)s * m + q] = p;
+        }
+    }
+    ECG_HIP(hipMemcpyAsync(t.dev, t.host, n * sizeof(void*), hipMemcpyHostToDevice, st));
+    const uint8_t* const* d_src = (const uint8_t* const*)t.dev;
+    uint8_t* const* d_dst = (uint8_t* const*)((const uint8_t**)t.dev + (size_t)S * k);
+    const int rc = run_ptrs(op, d_src, d_dst, S, B, aligned, st);
+    ECG_HIP(hipEventRecord(t.ev, st));
+    t.pending = true;
+    return rc;
+}
+
+int Engine::launch_direct(const std::vector<LinearOp>& ops, uint8_t* const* blocks, long long B, hipStream_t st) {
+    for (const LinearOp& op : ops) {
+        int rc = launch_one(op, blocks, B, st);
+        if (rc != ECG_OK) return rc;
+    }
+    return ECG_OK;
+}
+
 int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B,
                        hipStream_t st) {
     if (B < 0) return ECG_EINVAL;
@@ -241,11 +405,15 @@ int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks,
         for (int id : op.dst_ids)
             if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
     }
-    for (const LinearOp& op : ops) {
-        int rc = launch_one(op, blocks, B, st);
-        if (rc != ECG_OK) return rc;
+    if (t_defer.active) {
+        if (ops.empty() || B == 0) return ECG_OK;
+        std::shared_ptr<const std::vector<LinearOp>> shared;
+        if (!t_defer.q.empty() && same_ops(*t_defer.q.back().ops, ops)) shared = t_defer.q.back().ops;
+        else shared = std::make_shared<const std::vector<LinearOp>>(ops);
+        t_defer.q.push_back(DeferredCall{this, st, B, std::move(shared), std::vector<uint8_t*>(blocks, blocks + nblocks)});
+        return t_defer.q.size() >= kMaxDeferred ? batch_flush() : ECG_OK;
     }
-    return ECG_OK;
+    return launch_direct(ops, blocks, B, st);
 }
 
 // Host-buffer tier (the reference's per-stripe calls on host memory).  Device slots are assigned to the
@@ -256,6 +424,10 @@ int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks,
 // per block (each pageable copy is a driver-staged round trip).  Large calls copy block by block.
 int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B) {
     if (B < 0) return ECG_EINVAL;
+    if (!t_defer.q.empty()) {
+        const int rc = batch_flush();  // keep call order with deferred device calls
+        if (rc != ECG_OK) return rc;
+    }
     if (ops.empty() || B == 0) return ECG_OK;
     hipStream_t st = thread_stream();
     if (!st) return ECG_EHIP;
@@ -371,6 +543,10 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
     if (S < 0 || B < 0) return ECG_EINVAL;
     if (S == 0 || B == 0) return ECG_OK;  // empty batch: nothing to read or write
     if (!in_base || !out_base) return ECG_EINVAL;
+    if (!t_defer.q.empty()) {
+        const int rc = batch_flush();
+        if (rc != ECG_OK) return rc;
+    }
     if (progs.size() > 1 && !d_prog_of_stripe) return ECG_EINVAL;
     int status = ECG_OK;
     std::shared_ptr<ProgramSet> ps = program_set(progs, &status);
@@ -433,6 +609,10 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     if (S < 0 || B < 0 || prog.k_in() < 1 || prog.m_out() < 1) return ECG_EINVAL;
     if (S == 0 || B == 0) return ECG_OK;
     if (!h_in || !h_out) return ECG_EINVAL;
+    if (!t_defer.q.empty()) {
+        const int rc = batch_flush();
+        if (rc != ECG_OK) return rc;
+    }
     if (chunk < 1) chunk = 16;
     if (chunk > S) chunk = S;
     const int kin = prog.k_in(), mout = prog.m_out();

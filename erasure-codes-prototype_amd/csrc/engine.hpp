@@ -53,6 +53,9 @@ public:
                     const int* d_stripe_of = nullptr);
     int run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
                  bool aligned16, hipStream_t stream);
+    // One op over S calls' block pointers (host arrays): uploads the pointer tables, then run_ptrs.
+    int run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* const*>& call_blocks, long long B,
+                      hipStream_t stream);
 
     // Host-resident batch (block b of stripe s at h_in + s*in_sstride + b*in_bstride, likewise out):
     // a 3-slot pipeline of H2D (2-D copies of the blocks the program reads), kernel, D2H (the blocks
@@ -66,6 +69,8 @@ public:
     int device() const { return device_; }
     size_t cache_size();
 
+    int launch_direct(const std::vector<LinearOp>& ops, uint8_t* const* blocks, long long B, hipStream_t stream);
+
 private:
     explicit Engine(int device);
     int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream);
@@ -74,6 +79,17 @@ private:
     std::mutex mu_;
     std::unordered_map<std::string, std::shared_ptr<ProgramSet>> cache_;
 };
+
+// Deferred-batch scope of the calling thread (ecg_batch_begin / ecg_batch_end).  Inside a scope,
+// device-tier calls (run_device: ecg_dev_matrix_*, ErasureCode objects on HBM buffers) are recorded
+// instead of launched; batch_flush() launches each run of consecutive calls with the same plan and
+// block size on the same stream as ONE pointer-table launch per op, splitting a run where a call
+// touches a block an earlier call of the run writes (or writes one it reads).  Host-tier and batched
+// calls flush first, so call order is kept.
+int batch_begin();
+int batch_flush();
+int batch_end();
+bool batch_active();
 
 // Last HIP error seen by this thread (for diagnostics through the C ABI).
 const char* last_error_string();

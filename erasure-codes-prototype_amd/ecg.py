@@ -62,6 +62,7 @@ EXPORTS = [
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
     "ecg_jerasure_invert_matrix", "ecg_jerasure_matrix_multiply", "ecg_galois_region_xor",
     "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode", "ecg_jerasure_matrix_dotprod",
+    "ecg_batch_begin", "ecg_batch_flush", "ecg_batch_end",
     "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
     "ecg_encode_batch",
     "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
@@ -142,6 +143,9 @@ def lib():
     sig = {
         "ecg_last_error": ([], ctypes.c_char_p),
         "ecg_version": ([], I),
+        "ecg_batch_begin": ([], I),
+        "ecg_batch_flush": ([], I),
+        "ecg_batch_end": ([], I),
         "ecg_device_count": ([], I),
         "ecg_set_device": ([I], I),
         "ecg_free": ([P], None),
@@ -314,6 +318,24 @@ def jerasure_matrix_decode(k, m, matrix, row_k_ones, erasures, data, coding, siz
 
 
 # ------------------------------------------------------------------ tier 2 (device / batched)
+
+class batch:
+    """Deferred-batch scope (ecg_batch_begin / ecg_batch_end): per-stripe device-tier calls made by this
+    thread inside the `with` block are recorded and launched as batched pointer-table launches on exit."""
+
+    def __enter__(self):
+        _check(lib().ecg_batch_begin(), "batch_begin")
+        return self
+
+    def flush(self):
+        _check(lib().ecg_batch_flush(), "batch_flush")
+
+    def __exit__(self, exc_type, exc, tb):
+        rc = lib().ecg_batch_end()
+        if exc_type is None:
+            _check(rc, "batch_end")
+        return False
+
 
 def dev_matrix_encode(k, m, matrix, data, coding, B, stream=None):
     return _check(lib().ecg_dev_matrix_encode(k, m, _ints(matrix), _ptrs(data), _ptrs(coding), B, _stream(stream)),

@@ -91,6 +91,19 @@ int ecg_dev_matrix_encode(int k, int m, const int* matrix, char** d_data_ptrs, c
                           void* stream);
 int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const int* erasures, char** d_data_ptrs,
                           char** d_coding_ptrs, long long B, void* stream);
+/* Deferred-batch scope of the calling thread.  The reference issues one call per stripe
+ * (proxy.cpp:312-349); on HBM-resident blocks each such call is a separate small launch, bound by
+ * launch cost (~8 us per RS(10,4) call).  Between ecg_batch_begin() and ecg_batch_end(), device-tier
+ * calls of this thread (ecg_dev_matrix_* and ErasureCode handles in ECG_MEM_DEVICE mode) are only
+ * validated and recorded; ecg_batch_end() (or ecg_batch_flush()) launches every run of consecutive
+ * calls with the same plan, block size and stream as one pointer-table launch per op, asynchronously
+ * on that stream.  Outputs are defined once the flush's work completes on the stream.  A run is split
+ * where a call reads or writes a block an earlier call of the run writes, or writes one it reads
+ * (blocks compared by address: partially overlapping blocks are not allowed).  Host-tier and batched
+ * calls made inside the scope flush first.  Scopes do not nest (ECG_EINVAL). */
+int ecg_batch_begin(void);
+int ecg_batch_flush(void);
+int ecg_batch_end(void);
 /* Generic region product: out[dst_ids[p]] = XOR_j coef[p*k_in+j] * in[src_ids[j]] for S stripes,
  * in block b of stripe s at in_base + s*in_sstride + b*in_bstride (likewise out). */
 int ecg_matrix_apply_batch(int k_in, int m_out, const int* coef, const int* src_ids, const int* dst_ids,

@@ -818,3 +818,74 @@ def test_empty_inputs(ecg, oracle, torch_cuda):
     assert rc == ecg.ECG_EINVAL
     torch.cuda.synchronize()
     assert bool((guard == 7).all())
+
+
+# ------------------------------------------------------------------ deferred-batch scope (ecg_batch_begin / _end)
+
+def test_batch_scope_per_stripe_calls(ecg, oracle, torch_cuda):
+    """Per-stripe ErasureCode calls on HBM buffers inside a batch scope (the reference's one-call-per-
+    stripe loop, proxy.cpp:312-349) give the same bytes as the batched tier, and nothing is launched
+    before the scope ends."""
+    torch = torch_cuda
+    k, m, S, B = 10, 4, 48, 64 * 1024 + 16
+    n = k + m
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    st = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, 0xBA7C4)
+    ref = st.clone()
+    ecg.encode_batch(k, m, M, ref[:, :k], ref[:, k:])
+    st[:, k:] = 0x5A
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
+    with ecg.batch():
+        for s in range(S):
+            ec.encode([st[s, j] for j in range(k)], [st[s, k + i] for i in range(m)], B)
+        torch.cuda.synchronize()
+        assert bool((st[:, k:] == 0x5A).all()), "deferred calls ran before the scope ended"
+    torch.cuda.synchronize()
+    assert torch.equal(st, ref)
+    # decode: runs of 8 stripes share an erasure pattern (one batched launch per run)
+    lost = torch.empty((S, 2, B), dtype=torch.uint8, device="cuda")
+    pats = [[(s // 8) % n, (s // 8 + 5) % n] for s in range(S)]
+    for s in range(S):
+        for e in pats[s]:
+            st[s, e] = 0xEE
+    with ecg.batch():
+        for s in range(S):
+            ec.decode([st[s, j] for j in range(k)], [st[s, k + i] for i in range(m)], B, pats[s] + [-1], 2)
+    torch.cuda.synchronize()
+    assert torch.equal(st, ref)
+    host = ref[:3].cpu().numpy()
+    for s in range(3):
+        coding = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode(k, m, M, [host[s, j] for j in range(k)], coding, B)
+        assert all(np.array_equal(coding[i], host[s, k + i]) for i in range(m))
+
+
+def test_batch_scope_hazards_split_runs(ecg, torch_cuda):
+    """Calls with the same plan that depend on each other (a chain of galois_region_xor-like additions
+    through perform_addition) must keep their sequential meaning inside a scope."""
+    torch = torch_cuda
+    B, N = 4096 + 7, 12
+    bufs = torch.randint(0, 256, (N + 1, B), dtype=torch.uint8, device="cuda")
+    expect = bufs.cpu().numpy().copy()
+    for i in range(1, N + 1):
+        expect[i] ^= expect[i - 1]  # acc_i = in_i ^ acc_{i-1}, sequentially
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=4, m=2))
+    with ecg.batch():
+        for i in range(1, N + 1):
+            ec.perform_addition([bufs[i - 1], bufs[i]], [bufs[i]], B, 2, 1)
+    torch.cuda.synchronize()
+    assert np.array_equal(bufs.cpu().numpy(), expect)
+    # independent calls of the same plan, interleaved with a host-tier call (which flushes first)
+    a = torch.randint(0, 256, (6, B), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((3, B), dtype=torch.uint8, device="cuda")
+    h_src, h_dst = np.full(B, 3, np.uint8), np.full(B, 5, np.uint8)
+    with ecg.batch():
+        for i in range(3):
+            ec.perform_addition([a[2 * i], a[2 * i + 1]], [out[i]], B, 2, 1)
+        ecg.galois_region_xor(h_src, h_dst, B)
+        torch.cuda.synchronize()
+        assert torch.equal(out, a[0::2] ^ a[1::2])  # flushed by the host-tier call
+        with pytest.raises(ecg.EcgError):
+            ecg.batch().__enter__()  # scopes do not nest
+    assert (h_dst == 6).all()

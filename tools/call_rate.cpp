@@ -1,0 +1,103 @@
+// Per-call rate of the device tier (tuning tool): the reference's proxy makes ONE ErasureCode call per
+// stripe (proxy.cpp:312-349); with HBM-resident blocks each such call is one asynchronous launch.  This
+// measures how many per-stripe calls per second the C ABI sustains (host issue cost) and the resulting
+// data rate, against one batched launch over the same stripes.
+// Build: hipcc -O2 -std=c++17 -I../include tools/call_rate.cpp -L.../lib -lecg
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "ecg.h"
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));    \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+#define OK(x)                                                                            \
+    do {                                                                                 \
+        int r_ = (x);                                                                    \
+        if (r_ != 0) {                                                                   \
+            fprintf(stderr, "%s:%d rc=%d %s\n", __FILE__, __LINE__, r_, ecg_last_error()); \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+    const int k = 10, m = 4, n = k + m;
+    const int reps = argc > 1 ? atoi(argv[1]) : 3;
+    int* M = ecg_reed_sol_vandermonde_coding_matrix(k, m, 8);
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (long long B : {64LL << 10, 256LL << 10, 1LL << 20}) {
+        const int S = (int)std::min(4096LL, (16LL << 30) / (n * B));
+        uint8_t* buf;
+        CK(hipMalloc(&buf, (size_t)S * n * B));
+        OK(ecg_fill_random(buf, (long long)S * n * B, 1, 0, st));
+        std::vector<char*> ptrs((size_t)S * n);
+        for (int s = 0; s < S; s++)
+            for (int b = 0; b < n; b++) ptrs[(size_t)s * n + b] = (char*)(buf + ((size_t)s * n + b) * B);
+        ecg_coding_parameters cp{};
+        cp.k = k;
+        cp.m = m;
+        ecg_ec* ec = ecg_ec_factory(ECG_RS, &cp);
+        OK(ecg_ec_set_memory(ec, ECG_MEM_DEVICE, st));
+        for (int mode = 0; mode < 4; mode++) {
+            double best_host = 1e30;
+            float best_dev = 1e30f;
+            for (int r = 0; r < reps + 1; r++) {
+                CK(hipStreamSynchronize(st));
+                CK(hipEventRecord(e0, st));
+                const double t0 = now();
+                if (mode == 0) {
+                    for (int s = 0; s < S; s++)
+                        OK(ecg_dev_matrix_encode(k, m, M, &ptrs[(size_t)s * n], &ptrs[(size_t)s * n + k], B, st));
+                } else if (mode == 1) {
+                    for (int s = 0; s < S; s++)
+                        OK(ecg_ec_encode(ec, &ptrs[(size_t)s * n], &ptrs[(size_t)s * n + k], (int)B));
+                } else if (mode == 2) {
+                    OK(ecg_encode_batch(k, m, M, buf, n * B, B, buf + k * B, n * B, B, B, S, st));
+                } else {  // the per-stripe loop inside a deferred-batch scope
+                    OK(ecg_batch_begin());
+                    for (int s = 0; s < S; s++)
+                        OK(ecg_ec_encode(ec, &ptrs[(size_t)s * n], &ptrs[(size_t)s * n + k], (int)B));
+                    OK(ecg_batch_end());
+                }
+                const double t1 = now();
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r > 0) {
+                    best_host = std::min(best_host, t1 - t0);
+                    best_dev = std::min(best_dev, ms);
+                }
+            }
+            const char* names[4] = {"ecg_dev_matrix_encode per stripe", "ecg_ec_encode (device) per stripe",
+                                    "ecg_encode_batch (one launch)", "ecg_ec_encode per stripe, batch scope"};
+            const char* name = names[mode];
+            const double data = (double)S * k * B;
+            printf("B=%7lld S=%5d %-36s host %7.2f us/call  device %8.3f ms  %7.1f GiB/s data  (%5.1f%% of HBM peak)\n", B, S,
+                   name, best_host / (mode == 2 ? 1 : S) * 1e6, best_dev, data / (best_dev * 1e-3) / (1 << 30),
+                   (double)S * n * B / (best_dev * 1e-3) / 8e12 * 100);
+            fflush(stdout);
+        }
+        ecg_ec_destroy(ec);
+        CK(hipFree(buf));
+    }
+    ecg_free(M);
+    return 0;
+}
