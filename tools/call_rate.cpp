@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <tuple>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -97,6 +98,25 @@ int main(int argc, char** argv) {
         }
         ecg_ec_destroy(ec);
         CK(hipFree(buf));
+    }
+    // Host tier (synchronous calls on host buffers, the proxy's own buffers): latency per call from C++.
+    for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 1024}, {10, 4, 16384}, {10, 4, 65536}}) {
+        int* Mh = ecg_reed_sol_vandermonde_coding_matrix(kk, mm, 8);
+        std::vector<std::vector<char>> blocks(kk + mm, std::vector<char>(B, 1));
+        std::vector<char*> p(kk + mm);
+        for (int i = 0; i < kk + mm; i++) p[i] = blocks[i].data();
+        const int calls = 4000;
+        OK(ecg_jerasure_matrix_encode(kk, mm, 8, Mh, p.data(), p.data() + kk, B));
+        double t0 = now();
+        for (int c = 0; c < calls; c++) OK(ecg_jerasure_matrix_encode(kk, mm, 8, Mh, p.data(), p.data() + kk, B));
+        const double enc = (now() - t0) / calls * 1e6;
+        int er[2] = {2, -1};
+        t0 = now();
+        for (int c = 0; c < calls; c++) OK(ecg_jerasure_matrix_decode(kk, mm, 8, Mh, 1, er, p.data(), p.data() + kk, B));
+        const double dec = (now() - t0) / calls * 1e6;
+        printf("host tier RS(%d,%d) B=%6d  encode %6.1f us/call  decode %6.1f us/call\n", kk, mm, B, enc, dec);
+        fflush(stdout);
+        ecg_free(Mh);
     }
     ecg_free(M);
     return 0;
