@@ -22,8 +22,8 @@ Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line
               from the GPU over PCIe (H2D -> kernel -> D2H pipeline), for DESIGN.md.
 
 Multi-GPU: one process per GPU (torch.distributed.run), stripes sharded per rank (ecg_dist), no
-data-path collective: barrier + synchronize around the timed region, elapsed time max-reduced,
-per-rank parity checksums all-gathered.
+data-path collective: rank 0's coding plan broadcast before the run, barrier + synchronize around the
+timed region, elapsed time max-reduced, per-rank parity checksums all-gathered.
 """
 import argparse
 import json
@@ -130,13 +130,14 @@ def rs_encode_decode(a, r):
     B = a.block_size or (1 << 20)
     S = a.stripes or 4096
     n = k + m
-    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    # rank 0 plans (coding matrix, the 14 single-erasure patterns) and fans the plan out (RCCL broadcast)
+    M = D.broadcast_ints(ecg.reed_sol_vandermonde_coding_matrix(k, m) if r.rank == 0 else None, r, device="cuda")
+    patterns = [[e] for e in D.broadcast_ints(list(range(n)) if r.rank == 0 else None, r, device="cuda")]
     stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
     rebuilt = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
     first = r.rank * S  # weak scaling: rank r holds global stripes [r*S, (r+1)*S)
     ecg.fill_random(stripes, 0xEC0DE, word_offset=D.data_word_offset(first, n, B))
     pattern_of_stripe = (torch.arange(S, device="cuda", dtype=torch.int32) % n).contiguous()
-    patterns = [[e] for e in range(n)]
     data, coding = stripes[:, :k], stripes[:, k:]
 
     def step(ev=None):

@@ -2,8 +2,9 @@
 
 Stripes are independent (the proxy loops stripes with no cross-stripe state, proxy.cpp:312-399), so a
 batch of S_total stripes is partitioned into contiguous ranges, one per rank.  torch.distributed is
-used only around the data path: a barrier before/after the timed region, a MAX of elapsed times, a SUM
-of processed bytes and an all-gather of per-rank 64-bit parity checksums for a bit-exact verdict.
+used only around the data path: a broadcast of the coding plan from rank 0 (coding matrix, erasure
+patterns) before it, a barrier before/after the timed region, a MAX of elapsed times, a SUM of
+processed bytes and an all-gather of per-rank 64-bit parity checksums for a bit-exact verdict.
 Backend "nccl" (RCCL over xGMI) on GPUs, "gloo" in CPU tests.
 """
 from __future__ import annotations
@@ -83,6 +84,19 @@ def max_over_ranks(value: float, r: Rank, device="cpu") -> float:
 
 def sum_over_ranks(value: float, r: Rank, device="cpu") -> float:
     return _reduce(value, r, dist.ReduceOp.SUM, device)
+
+
+def broadcast_ints(vals, r: Rank, device="cpu", src: int = 0) -> list[int]:
+    """Fan out a small integer list (coding matrix, erasure patterns) from rank `src` to every rank;
+    other ranks pass None.  The only data-independent exchange before the timed region."""
+    if not r.distributed:
+        return list(vals)
+    n = torch.tensor([len(vals) if r.rank == src else 0], dtype=torch.int64, device=_dev(device))
+    dist.broadcast(n, src)
+    t = (torch.tensor(list(vals), dtype=torch.int64, device=_dev(device)) if r.rank == src
+         else torch.zeros(int(n.item()), dtype=torch.int64, device=_dev(device)))
+    dist.broadcast(t, src)
+    return [int(x) for x in t.tolist()]
 
 
 def checksum64(t: torch.Tensor) -> int:

@@ -50,8 +50,9 @@ def _worker(rank, world, port, total, q):
     sums = D.gather_checksums(c, r, device="cuda")
     t = D.max_over_ranks(float(rank + 1), r, device="cuda")
     n = D.sum_over_ranks(float(last - first), r, device="cuda")
+    plan = D.broadcast_ints([7, 1, 255, 0, 42] if rank == 0 else None, r, device="cuda")
     D.barrier(r)
-    q.put((rank, first, last, sums, t, n))
+    q.put((rank, first, last, sums, t, n, plan))
     torch.distributed.destroy_process_group()
 
 
@@ -76,6 +77,8 @@ def test_two_rank_sharding_matches_single_process(total):
     # max over ranks of (rank+1) and the sum of processed stripes
     assert res[0][4] == res[1][4] == 2.0
     assert res[0][5] == res[1][5] == float(total)
+    # the coding plan fanned out from rank 0
+    assert res[0][6] == res[1][6] == [7, 1, 255, 0, 42]
 
 
 def test_stripe_range_single_and_uneven():
