@@ -130,6 +130,45 @@ __global__ void __launch_bounds__(64 * W) xor_split(u32x4* __restrict__ st_base,
     }
 }
 
+// Two sequential streams at a read:write ratio R:W: workgroup u reads R x 2 KiB contiguous from `in`
+// at u*R*2K and writes W x 2 KiB contiguous to `out` at u*W*2K (the encode's 10:4 mix, no stripes).
+template <int R, int W>
+__global__ void __launch_bounds__(TPB) rw_ratio(const u32x4* __restrict__ in, u32x4* __restrict__ out) {
+    const long long u = xcd_map(blockIdx.x);
+    const u32x4* ip = in + u * R * TPB + threadIdx.x;
+    u32x4* op = out + u * W * TPB + threadIdx.x;
+    u32x4 x[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) x[j] = ld(ip + j * TPB);
+    u32x4 a = x[0];
+#pragma unroll
+    for (int j = 1; j < R; ++j) a ^= x[j];
+    if constexpr (W == 0) {
+        if ((a.x & a.y & a.z & a.w) == 0x12345678u) out[threadIdx.x] = a;
+    } else {
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+            u32x4 o = a;
+            o.x ^= p;
+            st(op + p * TPB, o);
+        }
+    }
+}
+
+// Stripe layout [S][K+M][B], K loads per lane, no stores (read side of the encode shape alone).
+template <int K, int M>
+__global__ void __launch_bounds__(TPB) stripe_read_only(const u32x4* __restrict__ st_base, u32x4* __restrict__ sink,
+                                                        long long B16, int wg_per_stripe) {
+    const long long w = xcd_map(blockIdx.x);
+    const long long s = w / wg_per_stripe;
+    const long long ch = w - s * wg_per_stripe;
+    const u32x4* sp = st_base + s * (K + M) * B16 + ch * TPB + threadIdx.x;
+    u32x4 a = ld(sp);
+#pragma unroll
+    for (int j = 1; j < K; ++j) a ^= ld(sp + j * B16);
+    if ((a.x & a.y & a.z & a.w) == 0x12345678u) sink[threadIdx.x] = a;
+}
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -243,6 +282,24 @@ int main(int argc, char** argv) {
         report("split W=10 xor 10r->1w dense", (double)S2 * 11 * B, ms);
         ms = T.med_ms([&] { xor_split<10, 4, 10><<<S * wps1, 640>>>(buf, sp, bp, wps1); }, reps);
         report("split W=10 xor 10r->4w dense", (double)S * 14 * B, ms);
+    }
+    {
+        // ratio experiments: regions A (reads) and B (writes) inside the 56 GiB buffer
+        const long long units = (S * 10 * B) / (10 * TPB * 16);  // 40 GiB of reads
+        const u32x4* A = buf;
+        u32x4* Bw = buf + units * 10 * TPB;
+        float ms = T.med_ms([&] { rw_ratio<10, 4><<<units, TPB>>>(A, Bw); }, reps);
+        report("two streams read:write 10:4", (double)units * 14 * TPB * 16, ms);
+        ms = T.med_ms([&] { rw_ratio<10, 1><<<units, TPB>>>(A, Bw); }, reps);
+        report("two streams read:write 10:1", (double)units * 11 * TPB * 16, ms);
+        ms = T.med_ms([&] { rw_ratio<10, 0><<<units, TPB>>>(A, Bw); }, reps);
+        report("one stream read 10 x 2 KiB per WG", (double)units * 10 * TPB * 16, ms);
+        ms = T.med_ms([&] { rw_ratio<1, 1><<<units, TPB>>>(A, Bw); }, reps);
+        report("two streams read:write 1:1", (double)units * 2 * TPB * 16, ms);
+        const long long B16 = B / 16;
+        const int wps = (int)(B16 / TPB);
+        ms = T.med_ms([&] { stripe_read_only<10, 4><<<S * wps, TPB>>>(buf, sink, B16, wps); }, reps);
+        report("stripes read-only 10 streams", (double)S * 10 * B, ms);
     }
     CK(hipFree(buf));
     CK(hipFree(sink));
