@@ -169,6 +169,35 @@ __global__ void __launch_bounds__(TPB) stripe_read_only(const u32x4* __restrict_
     if ((a.x & a.y & a.z & a.w) == 0x12345678u) sink[threadIdx.x] = a;
 }
 
+// Read/write phasing: every workgroup of a resident grid first reads J chunk-jobs (10 inputs each,
+// XOR-folded into registers), then writes their 4 outputs; one launch per slice of G*J jobs, so the
+// whole chip reads, then writes, then the next launch starts (kernel boundary = global barrier).
+template <int J>
+__global__ void __launch_bounds__(TPB) phased_10_4(u32x4* __restrict__ st_base, long long B16, int wg_per_stripe,
+                                                   long long job0) {
+    constexpr int K = 10, M = 4;
+    u32x4 acc[J];
+    u32x4* sp[J];
+#pragma unroll
+    for (int i = 0; i < J; ++i) {
+        const long long job = job0 + (long long)blockIdx.x * J + i;
+        const long long s = job / wg_per_stripe, ch = job - s * wg_per_stripe;
+        sp[i] = st_base + s * (K + M) * B16 + ch * TPB + threadIdx.x;
+        u32x4 a = ld(sp[i]);
+#pragma unroll
+        for (int j = 1; j < K; ++j) a ^= ld(sp[i] + j * B16);
+        acc[i] = a;
+    }
+#pragma unroll
+    for (int i = 0; i < J; ++i)
+#pragma unroll
+        for (int p = 0; p < M; ++p) {
+            u32x4 o = acc[i];
+            o.x ^= p;
+            st(sp[i] + (K + p) * B16, o);
+        }
+}
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -199,6 +228,7 @@ static void report(const char* name, double bytes, float ms) {
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 7;
+    const bool only_new = argc > 2 && atoi(argv[2]) == 1;  // 1: only the phasing experiment
     const long long B = 1ll << 20, S = 4096, K = 10, M = 4;
     const long long total = S * (K + M) * B;  // 56 GiB, the config-2 working set
     u32x4* buf;
@@ -211,6 +241,7 @@ int main(int argc, char** argv) {
     const long long n16 = half / 16;
     const u32x4* src = buf;
     u32x4* dst = buf + n16;
+    if (!only_new) {
     for (int u : {1, 2, 4, 8}) {
         const long long wgs = n16 / ((long long)u * TPB);
         char nm[64];
@@ -300,6 +331,35 @@ int main(int argc, char** argv) {
         const int wps = (int)(B16 / TPB);
         ms = T.med_ms([&] { stripe_read_only<10, 4><<<S * wps, TPB>>>(buf, sink, B16, wps); }, reps);
         report("stripes read-only 10 streams", (double)S * 10 * B, ms);
+    }
+    }  // !only_new
+    {
+        const long long B16 = B / 16;
+        const int wps = (int)(B16 / TPB);
+        const long long jobs = S * wps;
+        for (int G : {2048, 4096}) {
+            auto run = [&](auto kern, int J) {
+                const long long per = (long long)G * J;
+                for (long long j0 = 0; j0 < jobs; j0 += per) {
+                    const long long n = std::min(per, jobs - j0);
+                    kern<<<(unsigned)(n / J), TPB>>>(buf, B16, wps, j0);
+                }
+            };
+            char nm[96];
+            float ms;
+            ms = T.med_ms([&] { run(phased_10_4<1>, 1); }, reps);
+            snprintf(nm, sizeof nm, "phased G=%d J=1", G);
+            report(nm, (double)S * 14 * B, ms);
+            ms = T.med_ms([&] { run(phased_10_4<4>, 4); }, reps);
+            snprintf(nm, sizeof nm, "phased G=%d J=4", G);
+            report(nm, (double)S * 14 * B, ms);
+            ms = T.med_ms([&] { run(phased_10_4<8>, 8); }, reps);
+            snprintf(nm, sizeof nm, "phased G=%d J=8", G);
+            report(nm, (double)S * 14 * B, ms);
+            ms = T.med_ms([&] { run(phased_10_4<16>, 16); }, reps);
+            snprintf(nm, sizeof nm, "phased G=%d J=16", G);
+            report(nm, (double)S * 14 * B, ms);
+        }
     }
     CK(hipFree(buf));
     CK(hipFree(sink));
