@@ -889,3 +889,53 @@ def test_batch_scope_hazards_split_runs(ecg, torch_cuda):
         with pytest.raises(ecg.EcgError):
             ecg.batch().__enter__()  # scopes do not nest
     assert (h_dst == 6).all()
+
+
+# ------------------------------------------------------------------ randomized code parameters, every family
+
+def _random_configs(n, seed):
+    """Random valid parameters for every ECTYPE (divisibility kept so groups are whole; Cauchy LRCs with
+    g >= 2 since g = 1 needs the unpinned cbest_8 table)."""
+    rng = random.Random(seed)
+    out = []
+    while len(out) < n:
+        t = rng.randrange(10)
+        if t == 0:
+            p = dict(k=rng.randint(1, 40), m=rng.randint(1, 8))
+        elif t == 1:
+            x = rng.randint(2, 4)
+            p = dict(k=rng.randint(2, 12), m=rng.randint(1, 4), x=x, seri_num=rng.randrange(x))
+        elif t in (2, 5):  # Azure, Optimal-Cauchy: l | k
+            l = rng.randint(1, 4)
+            p = dict(k=l * rng.randint(2, 6), l=l, g=rng.randint(2 if t == 5 else 1, 4))
+        elif t == 3:       # Azure+1: (l - 1) | k
+            l = rng.randint(2, 4)
+            p = dict(k=(l - 1) * rng.randint(2, 6), l=l, g=rng.randint(1, 3))
+        elif t in (4, 6):  # Optimal, Uniform-Cauchy: l | (k + g)
+            l = rng.randint(1, 4)
+            g = rng.randint(2 if t == 6 else 1, 4)
+            kg = l * rng.randint(max(2, (g + 2 + l - 1) // l), 6)
+            p = dict(k=kg - g, l=l, g=g)
+        else:              # PC, HPC, HVPC
+            p = dict(k1=rng.randint(2, 5), m1=rng.randint(1, 2), k2=rng.randint(2, 4), m2=rng.randint(1, 2))
+            if t == 8:
+                p.update(x=rng.randint(2, 3), seri_num=0)
+                p["seri_num"] = rng.randrange(p["x"])
+        out.append((f"rand{len(out)}-{t}-{p}", t, p))
+    return out
+
+
+@pytest.mark.parametrize("name,t,params", _random_configs(60, 0xC0DE5))
+def test_random_codes_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
+    """Encode, decode (random patterns, garbage-free erased buffers) and partial encode/decode of
+    randomly drawn parameters of every code family, product vs oracle, byte for byte."""
+    from oracle import ec_ref as E
+    B = 1024 + 3
+    o, p = _pair(t, params)
+    data = E.blocks(o.k, B, 11)
+    ca, cb = E.zeros(o.m, B), E.zeros(o.m, B)
+    o.encode(data, ca, B)
+    assert p.encode(data, cb, B) == 0
+    assert same(ca, cb), name
+    test_facade_decode_vs_oracle(ecg, oracle, torch_cuda, name, t, params)
+    test_facade_partials_vs_oracle(ecg, oracle, torch_cuda, name, t, params)
