@@ -56,6 +56,8 @@ int ecg_set_device(int device) { return hipSetDevice(device) == hipSuccess ? ECG
 
 void ecg_free(void* p) { free(p); }
 
+int ecg_program_cache_size(void) { return (int)Engine::instance().cache_size(); }
+
 int ecg_batch_begin(void) { return batch_begin(); }
 int ecg_batch_flush(void) { return batch_flush(); }
 int ecg_batch_end(void) { return batch_end(); }

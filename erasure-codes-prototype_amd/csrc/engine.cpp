@@ -59,7 +59,11 @@ ThreadCtx& tctx(int device) { return t_ctx[device]; }
 const char* last_error_string() { return t_last_error.c_str(); }
 void set_last_error(const std::string& s) { t_last_error = s; }
 
+// A set is destroyed only after the cache dropped it AND every caller released it; kernels already
+// enqueued may still read its tables, so wait for the device before freeing (eviction is rare: at
+// most once per ECG_OPT_PROGRAM_CACHE / 2 new programs).
 ProgramSet::~ProgramSet() {
+    if (d_tabs || d_src || d_dst) (void)hipDeviceSynchronize();
     if (d_tabs) (void)hipFree(d_tabs);
     if (d_src) (void)hipFree(d_src);
     if (d_dst) (void)hipFree(d_dst);
@@ -122,7 +126,10 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
     {
         std::lock_guard<std::mutex> lk(mu_);
         auto it = cache_.find(key);
-        if (it != cache_.end()) return it->second;
+        if (it != cache_.end()) {
+            it->second.last_use = ++tick_;
+            return it->second.ps;
+        }
     }
     auto ps = std::make_shared<ProgramSet>();
     ps->nprog = np;
@@ -161,10 +168,34 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
         return fail(e, "hipMemcpy(src)");
     if ((e = hipMemcpy(ps->d_dst, dst.data(), dst.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "hipMemcpy(dst)");
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = cache_.find(key);
-    if (it != cache_.end()) return it->second;  // another thread won the race
-    cache_.emplace(std::move(key), ps);
+    std::vector<std::shared_ptr<ProgramSet>> evicted;  // destroyed outside the lock
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = cache_.find(key);
+        if (it != cache_.end()) {  // another thread won the race
+            it->second.last_use = ++tick_;
+            return it->second.ps;
+        }
+        const size_t cap = (size_t)std::max(2LL, get_option(ECG_OPT_PROGRAM_CACHE));
+        if (cache_.size() >= cap) {  // keep the cap / 2 most recently used programs
+            std::vector<uint64_t> uses;
+            uses.reserve(cache_.size());
+            for (auto& kv : cache_) uses.push_back(kv.second.last_use);
+            const size_t drop = cache_.size() - cap / 2;
+            std::nth_element(uses.begin(), uses.begin() + drop, uses.end());
+            const uint64_t cut = uses[drop];
+            for (auto i = cache_.begin(); i != cache_.end();) {
+                if (i->second.last_use < cut) {
+                    evicted.push_back(std::move(i->second.ps));
+                    i = cache_.erase(i);
+                } else {
+                    ++i;
+                }
+            }
+        }
+        cache_.emplace(std::move(key), CacheEntry{ps, ++tick_});
+    }
+    evicted.clear();
     return ps;
 }
 

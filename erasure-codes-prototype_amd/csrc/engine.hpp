@@ -76,8 +76,13 @@ private:
     int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream);
 
     int device_;
+    struct CacheEntry {
+        std::shared_ptr<ProgramSet> ps;
+        uint64_t last_use;
+    };
     std::mutex mu_;
-    std::unordered_map<std::string, std::shared_ptr<ProgramSet>> cache_;
+    uint64_t tick_ = 0;
+    std::unordered_map<std::string, CacheEntry> cache_;  // LRU-bounded by ECG_OPT_PROGRAM_CACHE
 };
 
 // Deferred-batch scope of the calling thread (ecg_batch_begin / ecg_batch_end).  Inside a scope,

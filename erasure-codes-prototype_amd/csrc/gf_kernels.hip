@@ -306,6 +306,7 @@ void init_options() {
     g_opt[ECG_OPT_COLS_PER_WG].store(env("ECG_COLS_PER_WG", 0));
     g_opt[ECG_OPT_GRID_MAP].store(env("ECG_GRID_MAP", 3));
     g_opt[ECG_OPT_ZEROCOPY_BYTES].store(env("ECG_ZEROCOPY_BYTES", 1 << 20));  // r01 host_latency.py
+    g_opt[ECG_OPT_PROGRAM_CACHE].store(env("ECG_PROGRAM_CACHE", 4096));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -387,6 +388,7 @@ int set_option(int opt, long long value) {
     if (opt == ECG_OPT_COLS_PER_WG && (value < 0 || (value % kThreads) != 0)) return -1;
     if (opt == ECG_OPT_GRID_MAP && (value < 0 || value > 3)) return -1;
     if (opt == ECG_OPT_ZEROCOPY_BYTES && value < 0) return -1;
+    if (opt == ECG_OPT_PROGRAM_CACHE && value < 2) return -1;
     g_opt[opt].store(value);
     return 0;
 }

@@ -36,7 +36,8 @@ ECG_OPT_NT = 0
 ECG_OPT_COLS_PER_WG = 1
 ECG_OPT_GRID_MAP = 2
 ECG_OPT_ZEROCOPY_BYTES = 3
-ECG_OPT_COUNT = 4
+ECG_OPT_PROGRAM_CACHE = 4
+ECG_OPT_COUNT = 5
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 
@@ -56,7 +57,7 @@ class RepairPlan:  # include/ec/erasure_code.h:53-58
 
 # Every symbol include/ecg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free",
+    "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free", "ecg_program_cache_size",
     "ecg_set_option", "ecg_get_option",
     "ecg_reed_sol_vandermonde_coding_matrix", "ecg_cauchy_good_general_coding_matrix",
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
@@ -143,6 +144,7 @@ def lib():
     sig = {
         "ecg_last_error": ([], ctypes.c_char_p),
         "ecg_version": ([], I),
+        "ecg_program_cache_size": ([], I),
         "ecg_batch_begin": ([], I),
         "ecg_batch_flush": ([], I),
         "ecg_batch_end": ([], I),

@@ -41,6 +41,7 @@ int ecg_version(void);             /* 100 * major + minor */
 int ecg_device_count(void);
 int ecg_set_device(int device);    /* selects the HIP device for the calling thread */
 void ecg_free(void* p);            /* frees matrices returned by this library (malloc'd, like Jerasure) */
+int ecg_program_cache_size(void);  /* programs cached for the current device (diagnostics) */
 
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
  * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP).  Results never depend on them. */
@@ -51,7 +52,10 @@ void ecg_free(void* p);            /* frees matrices returned by this library (m
 #define ECG_OPT_ZEROCOPY_BYTES 3 /* host-buffer calls whose staged blocks total at most this many bytes
                                     run the kernel on mapped pinned memory (no DMA); 0 = never;
                                     default 1 MiB */
-#define ECG_OPT_COUNT 4
+#define ECG_OPT_PROGRAM_CACHE 4 /* coefficient-table programs kept in HBM per device (LRU); when full, all
+                                   but the newest half are dropped (freed after a device synchronize).
+                                   Default 4096 */
+#define ECG_OPT_COUNT 5
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

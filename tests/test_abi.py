@@ -199,6 +199,8 @@ def test_tuning_options_validation(ecg):
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_NT, 4) != 0
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_COLS_PER_WG, 100) != 0  # not a multiple of the WG size
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_GRID_MAP, 4) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_PROGRAM_CACHE, 1) != 0
+        assert ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE) == saved[ecg.ECG_OPT_PROGRAM_CACHE]
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_COLS_PER_WG, 512) == 0
         assert ecg.get_option(ecg.ECG_OPT_COLS_PER_WG) == 512
     finally:

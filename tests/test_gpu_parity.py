@@ -939,3 +939,29 @@ def test_random_codes_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
     assert same(ca, cb), name
     test_facade_decode_vs_oracle(ecg, oracle, torch_cuda, name, t, params)
     test_facade_partials_vs_oracle(ecg, oracle, torch_cuda, name, t, params)
+
+
+def test_program_cache_bounded(ecg, oracle, torch_cuda):
+    """More distinct coefficient programs than ECG_OPT_PROGRAM_CACHE: the cache stays bounded (LRU half
+    dropped after a device synchronize) and every result stays exact, including launches still in
+    flight when their program is evicted."""
+    torch = torch_cuda
+    saved = ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE)
+    rng = random.Random(77)
+    k, m, B = 6, 3, 8192 + 16
+    try:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 8)
+        d = torch.empty((40, k + m, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(d, 0xCAC4E)
+        mats = [[rng.randrange(256) for _ in range(k * m)] for _ in range(40)]
+        for s in range(40):  # asynchronous launches, one new program each
+            ecg.encode_batch(k, m, mats[s], d[s:s + 1, :k], d[s:s + 1, k:])
+            assert ecg.lib().ecg_program_cache_size() <= 8
+        torch.cuda.synchronize()
+        host = d.cpu().numpy()
+        for s in range(40):
+            coding = [np.zeros(B, np.uint8) for _ in range(m)]
+            oracle.jerasure_matrix_encode(k, m, mats[s], [host[s, j] for j in range(k)], coding, B)
+            assert all(np.array_equal(coding[i], host[s, k + i]) for i in range(m)), s
+    finally:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
