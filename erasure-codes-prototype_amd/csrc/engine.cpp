@@ -33,8 +33,6 @@ struct ThreadCtx {
     hipStream_t stream = nullptr;
     uint8_t* scratch = nullptr;
     size_t cap = 0;
-    void** d_ptrs = nullptr;     // pointer tables for ops too wide for kernel arguments
-    size_t d_ptrs_cap = 0;
     // host-batch pipeline: 3 streams, 3 device slots
     hipStream_t pstream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t in_done[3] = {}, comp_done[3] = {}, out_done[3] = {};
@@ -199,25 +197,16 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
     return ps;
 }
 
-// One op over block pointers (device addresses), any k_in / m_out.
+// One op over block pointers (device addresses), any k_in / m_out.  Ops that fit the kernel arguments
+// carry their pointers inline; wider ones (k_in > 128 or m_out > 32) go through an uploaded pointer
+// table (run_ptr_batch with one call), still asynchronous.
 int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st) {
     if (op.m_out() == 0 || B == 0) return ECG_OK;
     if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
         for (int d : op.dst_ids) ECG_HIP(hipMemsetAsync(blocks[d], 0, (size_t)B, st));
         return ECG_OK;
     }
-    if (op.m_out() > kInlineDst) {  // split the outputs; every row reads the same inputs
-        for (int r0 = 0; r0 < op.m_out(); r0 += kInlineDst) {
-            LinearOp part;
-            part.src_ids = op.src_ids;
-            const int r1 = std::min(op.m_out(), r0 + kInlineDst);
-            part.dst_ids.assign(op.dst_ids.begin() + r0, op.dst_ids.begin() + r1);
-            part.coef.assign(op.coef.begin() + (size_t)r0 * op.k_in(), op.coef.begin() + (size_t)r1 * op.k_in());
-            int rc = launch_one(part, blocks, B, st);
-            if (rc != ECG_OK) return rc;
-        }
-        return ECG_OK;
-    }
+    if (op.k_in() > kInlineSrc || op.m_out() > kInlineDst) return run_ptr_batch(op, {blocks}, B, st);
     int status = ECG_OK;
     std::shared_ptr<ProgramSet> ps = program_set({op}, &status);
     if (!ps) return status;
@@ -236,31 +225,9 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     bool vec_ok = true;
     for (int d : op.dst_ids) vec_ok &= aligned16(blocks[d]);
     for (int s : op.src_ids) vec_ok &= aligned16(blocks[s]);
-    if (op.k_in() <= kInlineSrc) {
-        for (int j = 0; j < op.k_in(); j++) a.isrc[j] = blocks[op.src_ids[j]];
-        for (int p = 0; p < op.m_out(); p++) a.idst[p] = blocks[op.dst_ids[p]];
-        ECG_HIP(launch_gf(a, GF_MODE_INLINE, vec_ok, st));
-        return ECG_OK;
-    }
-    // Wide op: device pointer tables in per-thread scratch (synchronised before reuse).
-    ThreadCtx& c = tctx(device_);
-    const size_t need = (size_t)(op.k_in() + op.m_out());
-    ECG_HIP(hipStreamSynchronize(st));
-    if (c.d_ptrs_cap < need) {
-        if (c.d_ptrs) (void)hipFree(c.d_ptrs);
-        c.d_ptrs = nullptr;
-        c.d_ptrs_cap = 0;
-        ECG_HIP(hipMalloc(&c.d_ptrs, need * sizeof(void*)));
-        c.d_ptrs_cap = need;
-    }
-    std::vector<void*> h(need);
-    for (int j = 0; j < op.k_in(); j++) h[j] = blocks[op.src_ids[j]];
-    for (int p = 0; p < op.m_out(); p++) h[op.k_in() + p] = blocks[op.dst_ids[p]];
-    ECG_HIP(hipMemcpyAsync(c.d_ptrs, h.data(), need * sizeof(void*), hipMemcpyHostToDevice, st));
-    a.src_ptrs = (const uint8_t* const*)c.d_ptrs;
-    a.dst_ptrs = (uint8_t* const*)(c.d_ptrs + op.k_in());
-    ECG_HIP(launch_gf(a, GF_MODE_PTRS, vec_ok, st));
-    ECG_HIP(hipStreamSynchronize(st));  // h[] and the table must outlive the launch
+    for (int j = 0; j < op.k_in(); j++) a.isrc[j] = blocks[op.src_ids[j]];
+    for (int p = 0; p < op.m_out(); p++) a.idst[p] = blocks[op.dst_ids[p]];
+    ECG_HIP(launch_gf(a, GF_MODE_INLINE, vec_ok, st));
     return ECG_OK;
 }
 
