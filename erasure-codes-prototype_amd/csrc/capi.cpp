@@ -116,7 +116,7 @@ int ecg_galois_region_xor(char* src, char* dest, int nbytes) {
 }
 
 int ecg_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs, int size) {
-    if (w != 8 || k < 1 || m < 1 || !matrix || size < 0) return ECG_EINVAL;
+    if (w != 8 || k < 1 || m < 1 || !matrix || !data_ptrs || !coding_ptrs || size < 0) return ECG_EINVAL;
     LinearOp op = plan_matrix_encode(k, m, matrix);
     if (op.m_out() == 0) return ECG_OK;
     std::vector<uint8_t*> blocks((size_t)k + m);
@@ -155,7 +155,7 @@ int ecg_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int
 
 int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
                                char** coding_ptrs, int size) {
-    if (w != 8 || k < 1 || m < 1 || !matrix || !erasures || size < 0) return -1;
+    if (w != 8 || k < 1 || m < 1 || !matrix || !erasures || !data_ptrs || !coding_ptrs || size < 0) return -1;
     std::vector<LinearOp> ops;
     if (plan_matrix_decode(k, m, matrix, row_k_ones, erasures, ops) < 0) return -1;
     std::vector<uint8_t*> blocks((size_t)k + m);
@@ -169,7 +169,7 @@ int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones,
 
 int ecg_dev_matrix_encode(int k, int m, const int* matrix, char** d_data_ptrs, char** d_coding_ptrs, long long B,
                           void* stream) {
-    if (k < 1 || m < 1 || !matrix || B < 0) return ECG_EINVAL;
+    if (k < 1 || m < 1 || !matrix || !d_data_ptrs || !d_coding_ptrs || B < 0) return ECG_EINVAL;
     LinearOp op = plan_matrix_encode(k, m, matrix);
     if (op.m_out() == 0) return ECG_OK;
     std::vector<uint8_t*> blocks((size_t)k + m);
@@ -180,7 +180,7 @@ int ecg_dev_matrix_encode(int k, int m, const int* matrix, char** d_data_ptrs, c
 
 int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const int* erasures, char** d_data_ptrs,
                           char** d_coding_ptrs, long long B, void* stream) {
-    if (k < 1 || m < 1 || !matrix || !erasures || B < 0) return ECG_EINVAL;
+    if (k < 1 || m < 1 || !matrix || !erasures || !d_data_ptrs || !d_coding_ptrs || B < 0) return ECG_EINVAL;
     std::vector<LinearOp> ops;
     if (plan_matrix_decode(k, m, matrix, row_k_ones, erasures, ops) < 0) return ECG_EUNDECODABLE;
     std::vector<uint8_t*> blocks((size_t)k + m);

@@ -185,6 +185,10 @@ def test_bad_arguments(ecg):
     assert ec.perform_addition(bufs, bufs[:1], 16, 3, 2) == ecg.ECG_EINVAL  # 3 % 2 != 0, erasure_code.cpp:73
     assert ecg.lib().ecg_ec_factory(99, ecg.CodingParameters().to_c()) is None
     assert ecg.reed_sol_vandermonde_coding_matrix(4, 2, w=16) is None
+    L, M = ecg.lib(), ecg._ints(ecg.reed_sol_vandermonde_coding_matrix(4, 2))
+    assert L.ecg_jerasure_matrix_encode(4, 2, 8, M, None, None, 16) == ecg.ECG_EINVAL  # NULL block arrays
+    assert L.ecg_jerasure_matrix_decode(4, 2, 8, M, 1, ecg._ints([0, -1]), None, None, 16) == -1
+    assert L.ecg_dev_matrix_encode(4, 2, M, None, None, 16, None) == ecg.ECG_EINVAL
     op = ecg.ec_factory(ecg.ECTYPE.OPTIMAL_CAUCHY_LRC, ecg.CodingParameters(k=8, l=2, g=1))
     with pytest.raises(ecg.EcgError) as e:
         op.make_encoding_matrix()
