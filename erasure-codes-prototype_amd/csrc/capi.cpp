@@ -101,7 +101,8 @@ int ecg_jerasure_invert_matrix(int* mat, int* inv, int rows, int w) {
 }
 
 int* ecg_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int c2, int w) {
-    if (w != 8 || !m1 || !m2 || r1 < 1 || c2 < 1) return nullptr;
+    // Jerasure indexes m2 as c1 x c2 without checking c1 == r2; a mismatch is refused here
+    if (w != 8 || !m1 || !m2 || r1 < 1 || c1 < 1 || c2 < 1 || c1 != r2) return nullptr;
     return to_malloc(matrix_multiply(m1, m2, r1, c1, r2, c2));
 }
 
