@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs-encode-decode",
-                    choices=["rs-encode-decode", "lrc-repair", "pc-merge", "rs4m-waves", "rs-host"])
+                    choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "pc-merge", "rs4m-waves",
+                             "rs-host"])
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -190,6 +191,57 @@ def rs_encode_decode(a, r):
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line
+
+
+# ------------------------------------------------------------------------------- config 2, decode detail
+
+def rs_decode_patterns(a, r):
+    """RS(10,4), 1 MiB, 4096 stripes: jerasure_matrix_decode (row_k_ones = failed_num, rs.cpp:36) per
+    erasure pattern, SURVEY.md §8(d) C2: data loss e=0 (the row_k_ones XOR path: 10 blocks XORed),
+    parity loss e=10 (re-encode one row), the rotating single erasure, and 2 / 3 / 4 erasures."""
+    k, m = 10, 4
+    n = k + m
+    B = a.block_size or (1 << 20)
+    S = a.stripes or 4096
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(stripes, 0xEC0DE, word_offset=D.data_word_offset(r.rank * S, n, B))
+    ecg.encode_batch(k, m, M, stripes[:, :k], stripes[:, k:])
+    out = torch.empty((S, m, B), dtype=torch.uint8, device="cuda")
+    rot = (torch.arange(S, device="cuda", dtype=torch.int32) % n).contiguous()
+    cases = [("data e=0 (XOR path)", [[0]], None), ("parity e=10", [[10]], None),
+             ("rotating single e = s mod 14", [[e] for e in range(n)], rot),
+             ("2 erasures {1, 12}", [[1, 12]], None), ("3 erasures {0, 5, 11}", [[0, 5, 11]], None),
+             ("4 erasures {2, 3, 7, 13}", [[2, 3, 7, 13]], None)]
+    res = {}
+    idx = torch.arange(S, device="cuda")
+    for name, pats, pos in cases:
+        f = len(pats[0])
+        o = out[:, :f]
+
+        def step(ev=None, pats=pats, pos=pos, o=o):
+            if ev:
+                ev[0].record()
+            ecg.decode_batch(k, m, M, f, pats, stripes, out=o, pattern_of_stripe=pos)
+            if ev:
+                ev[1].record()
+
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        if pos is None:  # written blocks come back in the library's write order (erased data, then coding)
+            order = sorted(x for x in pats[0] if x < k) + sorted(x for x in pats[0] if x >= k)
+            for i, e in enumerate(order):
+                assert torch.equal(o[:, i], stripes[:, e]), f"{name}: block {e} mismatch"
+        else:
+            assert torch.equal(o[:, 0], stripes[idx, idx % n]), f"{name}: mismatch"
+        elapsed, evs = timed_loop(r, a.steps, step)
+        t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+        alg = S * (k + f) * B  # reads k survivors, writes f blocks
+        res[name] = {"ms": round(t * 1e3, 3), "data_GiBps": round(r.world * S * k * B / t / 2 ** 30, 1),
+                     "algorithmic_GBps": round(alg / t / 1e9, 1), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+    return {"workload": "RS(10,4) 1 MiB decode by erasure pattern, 4096 stripes", "n_gpus": r.world,
+            "results": res, "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
 # ------------------------------------------------------------------------------- config 3
@@ -474,7 +526,7 @@ def main():
     else:
         D.init(r, "nccl", device=torch.device("cuda", dev) if r.distributed else None)
     ecg.lib().ecg_set_device(torch.cuda.current_device())
-    fn = {"rs-encode-decode": rs_encode_decode, "lrc-repair": lrc_repair, "pc-merge": pc_merge,
+    fn = {"rs-encode-decode": rs_encode_decode, "rs-decode-patterns": rs_decode_patterns, "lrc-repair": lrc_repair, "pc-merge": pc_merge,
           "rs4m-waves": rs4m_waves, "rs-host": rs_host}[a.workload]
     line = fn(a, r)
     if r.rank == 0:
