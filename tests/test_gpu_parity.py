@@ -965,3 +965,39 @@ def test_program_cache_bounded(ecg, oracle, torch_cuda):
             assert all(np.array_equal(coding[i], host[s, k + i]) for i in range(m)), s
     finally:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
+
+
+def test_large_host_blocks_pinned_for_the_call(ecg, oracle, torch_cuda):
+    """The reference's SET buffers (proxy.cpp:335-339): k slices of ONE contiguous value buffer and m
+    separate parity buffers, 1 MiB blocks.  The host tier pins them for the call (refcounted, so four
+    threads encoding from the same value buffer never unpin each other's pages) and returns the bytes
+    the oracle computes; the buffers stay ordinary pageable memory afterwards."""
+    k, m, B = 10, 4, 1 << 20
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    value = rnd(k * B, 4242)
+    data = [value[j * B:(j + 1) * B] for j in range(k)]
+    expect = [np.zeros(B, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, data, expect, B)
+    outs = [[np.zeros(B, np.uint8) for _ in range(m)] for _ in range(4)]
+    errs = []
+
+    def work(t):
+        try:
+            for _ in range(3):
+                ecg.jerasure_matrix_encode(k, m, M, data, outs[t], B)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    assert not errs, errs
+    for t in range(4):
+        assert same(outs[t], expect), t
+    # decode in place: lose data 3 and parity 1 (garbage in both), survivors are slices of `value`
+    stripe = data + [x.copy() for x in expect]
+    lost = [stripe[3].copy(), stripe[k + 1].copy()]
+    stripe[3][:] = 0xEE
+    stripe[k + 1][:] = 0xEE
+    assert ecg.jerasure_matrix_decode(k, m, M, 2, [3, k + 1, -1], stripe[:k], stripe[k:], B) == 0
+    assert np.array_equal(stripe[3], lost[0]) and np.array_equal(stripe[k + 1], lost[1])

@@ -100,12 +100,16 @@ int main(int argc, char** argv) {
         CK(hipFree(buf));
     }
     // Host tier (synchronous calls on host buffers, the proxy's own buffers): latency per call from C++.
-    for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 1024}, {10, 4, 16384}, {10, 4, 65536}}) {
+    for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 1024}, {10, 4, 16384}, {10, 4, 65536},
+                             {10, 4, 1 << 20}, {10, 4, 4 << 20}}) {
         int* Mh = ecg_reed_sol_vandermonde_coding_matrix(kk, mm, 8);
-        std::vector<std::vector<char>> blocks(kk + mm, std::vector<char>(B, 1));
+        // the proxy's SET buffers (proxy.cpp:335-339): data = slices of one value buffer, parities separate
+        std::vector<char> value((size_t)kk * B, 1);
+        std::vector<std::vector<char>> blocks(mm, std::vector<char>(B, 1));
         std::vector<char*> p(kk + mm);
-        for (int i = 0; i < kk + mm; i++) p[i] = blocks[i].data();
-        const int calls = 4000;
+        for (int i = 0; i < kk; i++) p[i] = value.data() + (size_t)i * B;
+        for (int i = 0; i < mm; i++) p[kk + i] = blocks[i].data();
+        const int calls = B >= (1 << 20) ? 100 : 4000;
         OK(ecg_jerasure_matrix_encode(kk, mm, 8, Mh, p.data(), p.data() + kk, B));
         double t0 = now();
         for (int c = 0; c < calls; c++) OK(ecg_jerasure_matrix_encode(kk, mm, 8, Mh, p.data(), p.data() + kk, B));
