@@ -341,6 +341,67 @@ struct Loopback::Impl {
         return true;
     }
 
+    // Proxy::decode_and_get_object's degraded read (proxy.cpp:517-666): partitions from the placement,
+    // generate_repair_plan over the unreachable data blocks, fetch the plan's help blocks, then ONE
+    // ec->decode with local_or_column = false (:564) and the unreachable blocks as erasures.
+    // Two reference defects are fixed, not copied:
+    //   * the reference fetches only the plan's help blocks but decodes GLOBALLY, so for a local plan
+    //     (LRC single loss) the global decode reads coding buffers it never fetched (zeros); here the
+    //     decode's own read set is fetched too: the first k surviving blocks (jerasure_matrix_decode),
+    //     or every surviving block for the product codes' iterative decode;
+    //   * proxy.cpp:673-677 never puts the rebuilt blocks into the returned value (a degraded GET there
+    //     is short); here they are.
+    bool degraded_read(Stripe& s, const std::vector<int>& obj_blocks, const std::vector<int>& missing,
+                       std::vector<char>& value) {
+        const size_t B = schema.block_size;
+        const int n = s.k + s.m;
+        std::vector<int> failures;
+        for (int j : missing) failures.push_back(obj_blocks[j]);
+        find_out_stripe_partitions(s);
+        std::vector<Plan> plans;
+        if (!plans_of(s, failures, plans)) return false;
+        std::vector<Block> data(s.k, Block(B, 0)), coding(s.m, Block(B, 0));
+        std::vector<char> have(n, 0), lost(n, 0), want(n, 0);
+        for (int f : failures) lost[f] = 1;
+        for (size_t j = 0; j < obj_blocks.size(); j++) {  // blocks the GET already read
+            const int b = obj_blocks[j];
+            if (lost[b]) continue;
+            memcpy((b < s.k ? data[b] : coding[b - s.k]).data(), value.data() + j * B, B);
+            have[b] = 1;
+        }
+        for (auto& p : plans)
+            for (auto& h : p.help)
+                for (int b : h) want[b] = 1;
+        if (is_pc(schema.ec_type)) {
+            for (int b = 0; b < n; b++) want[b] |= !lost[b];
+        } else {
+            for (int b = 0, got = 0; b < n && got < s.k; b++)
+                if (!lost[b]) {
+                    want[b] = 1;
+                    got++;
+                }
+        }
+        for (int b = 0; b < n; b++) {
+            if (!want[b] || have[b] || lost[b]) continue;
+            if (!read(BlockLoc{b, s.block_ids[b], s.blocks2nodes[b]}, B, b < s.k ? data[b] : coding[b - s.k]))
+                return false;
+            have[b] = 1;
+        }
+        ecg_coding_parameters saved{};
+        ecg_ec_get_coding_parameters(s.ec, &saved);
+        ecg_coding_parameters cp = saved;
+        cp.local_or_column = 0;  // proxy.cpp:564
+        ecg_ec_init_coding_parameters(s.ec, &cp);
+        std::vector<int> erasures = failures;
+        erasures.push_back(-1);
+        auto dp = ptrs(data), cpp = ptrs(coding);
+        const int rc = ecg_ec_decode(s.ec, dp.data(), cpp.data(), (int)B, erasures.data(), (int)failures.size());
+        ecg_ec_init_coding_parameters(s.ec, &saved);
+        if (!ok(rc)) return false;
+        for (int j : missing) memcpy(value.data() + j * B, data[obj_blocks[j]].data(), B);
+        return true;
+    }
+
     // repair.cpp:190-470 concrete_repair_plans / concrete_repair_plans_pc
     bool concretise(Stripe& s, const Plan& plan, RepairCall& main, std::vector<RepairCall>& helps) {
         const int main_cid = topo.cluster_of(s.blocks2nodes[plan.failures[0]]);
@@ -705,14 +766,35 @@ bool Loopback::get(const std::string& key, std::vector<char>& value) {
     const std::vector<int>& blocks = it->second.second;
     const size_t B = I.schema.block_size;
     value.assign(blocks.size() * B, 0);
+    std::vector<int> missing;  // positions in the value whose data block is unreachable
     for (size_t j = 0; j < blocks.size(); j++) {
         const int b = blocks[j];
         if (!I.store.access_data(I.topo.node_port(s.blocks2nodes[b]), key_of(s.block_ids[b]), value.data() + j * B, B))
-            return false;
+            missing.push_back((int)j);
+    }
+    if (!missing.empty()) {
+        if (!I.degraded_read(stripes_.at(it->second.first), blocks, missing, value)) return false;
+        stats.degraded_gets++;
     }
     stats.gets++;
     stats.get_s += now_s() - t0;
     return true;
+}
+
+bool Loopback::get_with_unreachable(const std::string& key, int data_pos, std::vector<char>& value) {
+    Impl& I = *impl_;
+    auto it = objects_.find(key);
+    if (it == objects_.end() || data_pos < 0 || data_pos >= (int)it->second.second.size()) return false;
+    const Stripe& s = stripes_.at(it->second.first);
+    const int b = it->second.second[data_pos];
+    const size_t B = I.schema.block_size;
+    const int port = I.topo.node_port(s.blocks2nodes[b]);
+    Block keep(B);
+    if (!I.store.access_data(port, key_of(s.block_ids[b]), keep.data(), B)) return false;
+    I.store.remove_data(port, key_of(s.block_ids[b]));  // the datanode is unreachable
+    const bool got = get(key, value);
+    I.store.store_data(port, key_of(s.block_ids[b]), keep.data(), B);
+    return got;
 }
 
 bool Loopback::repair(unsigned stripe_id, const std::vector<int>& failures) {

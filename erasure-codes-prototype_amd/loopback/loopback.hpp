@@ -54,7 +54,7 @@ struct Stripe {
 };
 
 struct Stats {
-    long sets = 0, gets = 0, get_mismatch = 0;
+    long sets = 0, gets = 0, get_mismatch = 0, degraded_gets = 0;
     long repairs = 0, repairs_failed = 0, repairs_skipped_undecodable = 0, repair_plans = 0, plans_partial = 0, plans_direct = 0;
     long blocks_rebuilt = 0, rebuilt_mismatch = 0;
     long helper_messages = 0, helper_bytes = 0;
@@ -78,8 +78,11 @@ public:
 
     // client.set (proxy.cpp:274-427): one stripe per object of k * block_size bytes
     bool set(const std::string& key, const std::vector<char>& value);
-    // client.get (proxy.cpp:428-724): the object's data blocks, concatenated
+    // client.get (proxy.cpp:428-724): the object's data blocks, concatenated; a data block whose datanode
+    // does not answer is rebuilt by the degraded read (proxy.cpp:517-666)
     bool get(const std::string& key, std::vector<char>& value);
+    // get() while the datanode of the object's data block `data_pos` is unreachable (block restored after)
+    bool get_with_unreachable(const std::string& key, int data_pos, std::vector<char>& value);
     // client.blocks_repair (repair.cpp:5-155): returns false if the code cannot repair the set
     bool repair(unsigned stripe_id, const std::vector<int>& failures);
     // client.merge: RS, Azure LRC, PC / HVPC / HPC (horizontal), as do_stripe_merge dispatches them

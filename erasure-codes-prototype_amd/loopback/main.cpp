@@ -4,7 +4,8 @@
 //
 //   set every object -> single-block repair of every block of every stripe -> 5 multi-block repairs
 //   (2..4 random failures) per stripe -> merge x stripes -> the same repairs on the merged stripes ->
-//   get every object and compare.
+//   degraded reads (one data block's datanode unreachable) of --degraded objects -> get every object
+//   and compare.
 //
 // Objects are splitmix64 bytes (word w of object j = splitmix64(seed + (j*k*B/8 + w) * golden)) instead
 // of the reference's one-character values (utils.cpp:92), which would hide multiply errors.
@@ -90,7 +91,7 @@ void usage() {
     fprintf(stderr,
             "ecg_loopback [--ec RS] [--k 6 --m 4 | --k --l --g | --k1 --m1 --k2 --m2] [--block-size 1024]\n"
             "             [--stripes 64] [--x 2] [--placement OPTIMAL] [--partial 1] [--store kv|disk]\n"
-            "             [--dir ./storage] [--seed 1] [--multi 5] [--no-merge] [--manifest path]\n");
+            "             [--dir ./storage] [--seed 1] [--multi 5] [--degraded 8] [--no-merge] [--manifest path]\n");
 }
 
 }  // namespace
@@ -99,7 +100,7 @@ int main(int argc, char** argv) {
     EcSchema schema;
     schema.cp.k = 6;
     schema.cp.m = 4;
-    int stripes = 64, multi = 5;
+    int stripes = 64, multi = 5, degraded = 8;
     bool do_merge = true;
     std::string store_kind = "kv", dir = "./storage", manifest;
     uint64_t seed = 1;
@@ -130,6 +131,7 @@ int main(int argc, char** argv) {
         else if (a == "--dir") dir = val();
         else if (a == "--seed") seed = strtoull(val().c_str(), nullptr, 0);
         else if (a == "--multi") multi = atoi(val().c_str());
+        else if (a == "--degraded") degraded = atoi(val().c_str());
         else if (a == "--no-merge") do_merge = false;
         else if (a == "--manifest") manifest = val();
         else if (a == "--selftest-store") return selftest_store(store_kind, dir);
@@ -192,6 +194,16 @@ int main(int argc, char** argv) {
         // matrix in the reference; they are not run.
         if (schema.ec_type != ECG_HIERACHICAL_PC) repairs(post_single, post_multi);
     }
+    // degraded reads (proxy.cpp:517-666): the datanode of one random data block of an object does not
+    // answer; the GET rebuilds it through ec->decode
+    long degraded_ok = 0, degraded_tried = 0;
+    for (int j = 0; j < std::min(degraded, (int)keys.size()); j++) {
+        std::vector<char> v;
+        const int pos = (int)(rng() % schema.cp.k);
+        degraded_tried++;
+        if (lb.get_with_unreachable(keys[j], pos, v) && v == object_bytes(seed, (uint64_t)j * value_len / 8, value_len))
+            degraded_ok++;
+    }
     // get
     long get_ok = 0;
     for (size_t j = 0; j < keys.size(); j++) {
@@ -210,13 +222,15 @@ int main(int argc, char** argv) {
            "\"plans_partial\": %ld, \"plans_direct\": %ld, \"blocks_rebuilt\": %ld, \"rebuilt_mismatch\": %ld, "
            "\"helper_messages\": %ld, \"helper_bytes\": %ld, \"merged\": %s, \"merges\": %ld, "
            "\"merged_parities\": %ld, \"final_stripes\": %zu, \"gets_ok\": %ld, \"get_mismatch\": %ld, "
+           "\"degraded_gets\": %ld, \"degraded_ok\": %ld, "
            "\"ecg_errors\": %ld, \"decode_undecodable\": %ld, \"blocks_in_store\": %zu, \"seconds\": {\"set\": %.4f, \"repair\": %.4f, "
            "\"merge\": %.4f, \"get\": %.4f}, \"mismatches\": %s}\n",
            schema.ec_type, schema.cp.k, schema.cp.m, schema.block_size, stripes, store_kind.c_str(),
            schema.partial_decoding ? "true" : "false", s.sets, s.repairs, pre_single, pre_multi, post_single,
            post_multi, s.repairs_failed, s.repairs_skipped_undecodable, s.repair_plans, s.plans_partial, s.plans_direct,
            s.blocks_rebuilt, s.rebuilt_mismatch, s.helper_messages, s.helper_bytes, merged ? "true" : "false",
-           s.merges, s.merged_parities, lb.list_stripes().size(), get_ok, s.get_mismatch, s.ecg_errors,
+           s.merges, s.merged_parities, lb.list_stripes().size(), get_ok, s.get_mismatch, degraded_tried, degraded_ok,
+           s.ecg_errors,
            s.decode_undecodable, store->count(), s.set_s, s.repair_s, s.merge_s, s.get_s, lb.mismatches_json().c_str());
     // exit status: 0 = every repair rebuilt the lost bytes; mismatches are listed for the checker
     const bool pass = s.rebuilt_mismatch == 0 && s.get_mismatch == 0 && s.ecg_errors == 0 &&

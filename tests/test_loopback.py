@@ -59,6 +59,8 @@ def test_config1_rs64_kv_store():
     assert s["rebuilt_mismatch"] == 0 and s["ecg_errors"] == 0 and s["repairs_failed"] == 0
     assert s["plans_partial"] > 0 and s["helper_messages"] > 0  # partial decoding crossed the "wire"
     assert s["blocks_in_store"] == 32 * 16  # old parities deleted, new ones written
+    # degraded reads (proxy.cpp:517-666): one data block's datanode unreachable, rebuilt by ec->decode
+    assert s["degraded_gets"] == 8 and s["degraded_ok"] == 8
 
 
 @pytest.mark.gpu
@@ -222,3 +224,7 @@ def test_other_codes_repair_and_get(code, args, partial, oracle):
         assert cauchy_quirk or ers_quirk or _undecodable(code, params, mm["failures"], oracle), mm
     if code in ("RS", "PC", "HV_PC") or (code == "Hierachical_PC" and partial == "1"):
         assert s["rebuilt_mismatch"] == 0 and s["decode_undecodable"] == 0, s["mismatches"]
+    # degraded GET (proxy.cpp:517-666, global decode of one unreachable data block): exact for every
+    # family (a single data loss with coding row 0 intact takes Jerasure's all-ones-row XOR shortcut, so
+    # even HPC's ERS columns decoded with the plain Vandermonde matrix come out right)
+    assert s["degraded_gets"] == 6 and s["degraded_ok"] == 6, s
