@@ -75,3 +75,46 @@ def test_shim_bytes(consumer, oracle, tmp_path, k, m, B):
     oracle.jerasure_matrix_encode(nloc, 1, R[:nloc], [blocks[i + 1] for i in range(nloc)], part, B)
     assert np.array_equal(got[m + 2], part[0]), "partial"
     assert np.array_equal(got[m + 3], data[0] ^ data[1]), "galois_region_xor"
+
+
+FACADE = os.path.join(PKG, "bin", "facade_consumer")
+
+
+@pytest.fixture(scope="module")
+def facade_consumer(ecg):
+    if not os.path.exists(FACADE):
+        subprocess.check_call(["make", "-s", "-C", PKG, "bin/facade_consumer"])
+    return FACADE
+
+
+def test_facade_cpp_plans(facade_consumer):
+    """INTEGRATION.md Option B compiles and links: ecg::ec_factory + the C++ classes, no GPU needed for
+    matrices and repair planning (Azure-LRC(12,2,2), block 0, OPTIMAL partition)."""
+    from oracle import ec_ref as E
+    out = subprocess.run([facade_consumer, "plans"], capture_output=True, text=True, check=True).stdout.splitlines()
+    M = [int(x) for x in out[0].split()[1:]]
+    assert M == E.ec_factory(E.ECTYPE.AZURE_LRC, E.CodingParameters(k=12, l=2, g=2)).make_encoding_matrix()
+    plan = out[1].split("|")
+    assert plan[0].split() == ["plan", "1"]  # a local plan
+    assert [sorted(int(x) for x in h.split()) for h in plan[1:]] == [[1, 2], [3, 4, 5], [14]]
+
+
+@pytest.mark.gpu
+def test_facade_cpp_bytes(facade_consumer, oracle, tmp_path):
+    """The same consumer on the GPU: Azure(12,2,2) encode and the partial-decoding repair of block 0
+    (helper partial + main partial + perform_addition) byte-for-byte against the oracle."""
+    from oracle import ec_ref as E
+    B = 65536 + 5
+    data = np.random.default_rng(12).integers(0, 256, (12, B), dtype=np.uint8)
+    inp, outp = tmp_path / "in.bin", tmp_path / "out.bin"
+    data.tofile(inp)
+    p = subprocess.run([facade_consumer, "bytes", str(inp), str(outp), str(B)], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    got = np.fromfile(outp, dtype=np.uint8).reshape(5, B)
+    ec = E.ec_factory(E.ECTYPE.AZURE_LRC, E.CodingParameters(k=12, l=2, g=2))
+    coding = E.zeros(4, B)
+    ec.encode(list(data), coding, B)
+    for i in range(4):
+        assert np.array_equal(got[i], coding[i]), i
+    assert np.array_equal(got[4], data[0])
