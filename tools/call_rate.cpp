@@ -5,7 +5,9 @@
 // Build: hipcc -O2 -std=c++17 -I../include tools/call_rate.cpp -L.../lib -lecg
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <tuple>
 #include <cstdio>
 #include <cstdlib>
@@ -120,6 +122,31 @@ int main(int argc, char** argv) {
         const double dec = (now() - t0) / calls * 1e6;
         printf("host tier RS(%d,%d) B=%6d  encode %6.1f us/call  decode %6.1f us/call\n", kk, mm, B, enc, dec);
         fflush(stdout);
+        ecg_free(Mh);
+    }
+    // Concurrent host-tier callers (the proxy runs encode on detached threads, proxy.cpp:416-419):
+    // T threads, each with its own buffers, issuing synchronous RS(6,4) / RS(10,4) calls.
+    for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 65536}}) {
+        int* Mh = ecg_reed_sol_vandermonde_coding_matrix(kk, mm, 8);
+        for (int T : {1, 2, 4, 8, 16}) {
+            const int calls = 2000;
+            std::vector<std::thread> th;
+            std::atomic<int> errors{0};
+            const double t0 = now();
+            for (int t = 0; t < T; t++)
+                th.emplace_back([&, t] {
+                    std::vector<std::vector<char>> blocks(kk + mm, std::vector<char>(B, (char)t));
+                    std::vector<char*> p(kk + mm);
+                    for (int i = 0; i < kk + mm; i++) p[i] = blocks[i].data();
+                    for (int c = 0; c < calls; c++)
+                        if (ecg_jerasure_matrix_encode(kk, mm, 8, Mh, p.data(), p.data() + kk, B) != 0) errors++;
+                });
+            for (auto& x : th) x.join();
+            const double dt = now() - t0;
+            printf("host tier RS(%d,%d) B=%6d  %2d threads: %8.0f calls/s  (%.1f us/call/thread)%s\n", kk, mm, B, T,
+                   T * calls / dt, dt / calls * 1e6, errors ? "  ERRORS" : "");
+            fflush(stdout);
+        }
         ecg_free(Mh);
     }
     ecg_free(M);
