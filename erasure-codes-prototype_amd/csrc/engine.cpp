@@ -52,56 +52,6 @@ thread_local ThreadCtx t_ctx[kMaxDevices];
 
 ThreadCtx& tctx(int device) { return t_ctx[device]; }
 
-// Pinning of caller-owned pageable host buffers for the duration of one call (large host-tier blocks,
-// pageable host batches).  A pageable copy is staged by the driver (per-block 1 MiB copies ran at ~23
-// GB/s); registering the caller's pages lets the DMA engines read them directly (~44 GB/s, the same as
-// pinned memory: tools/pageable_copy.cpp).  Safety rules:
-//   * one pinned call at a time process-wide (g_pin_mu, held for the whole call): registrations made
-//     here never overlap, and no call can unregister pages another call is still transferring (one
-//     call already saturates PCIe, so concurrent large host calls lose nothing by queueing);
-//   * a call's blocks are merged at PAGE granularity, so two of its blocks sharing a page become one
-//     registration;
-//   * a range the runtime refuses (e.g. already registered by the caller) is left as it is and copied
-//     the runtime's own way, exactly as without pinning;
-//   * the destructor synchronises the call's streams before unregistering, so an early error return
-//     never unpins pages a copy is still using.
-std::mutex g_pin_mu;
-
-struct PinnedCall {
-    std::unique_lock<std::mutex> lk;
-    std::vector<hipStream_t> streams;
-    std::vector<uintptr_t> regs;  // page-aligned starts of the ranges registered by this call
-
-    PinnedCall(std::vector<hipStream_t> s, std::vector<std::pair<uintptr_t, uintptr_t>> spans)
-        : lk(g_pin_mu), streams(std::move(s)) {
-        const uintptr_t pg = 4096;
-        for (auto& sp : spans) {
-            sp.first &= ~(pg - 1);
-            sp.second = (sp.second + pg - 1) & ~(pg - 1);
-        }
-        std::sort(spans.begin(), spans.end());
-        std::vector<std::pair<uintptr_t, uintptr_t>> merged;
-        for (auto& sp : spans) {
-            if (sp.first >= sp.second) continue;
-            if (!merged.empty() && sp.first <= merged.back().second)
-                merged.back().second = std::max(merged.back().second, sp.second);
-            else
-                merged.push_back(sp);
-        }
-        for (auto& r : merged) {
-            if (hipHostRegister((void*)r.first, r.second - r.first, hipHostRegisterDefault) == hipSuccess)
-                regs.push_back(r.first);
-            else
-                (void)hipGetLastError();
-        }
-    }
-    ~PinnedCall() {
-        if (regs.empty()) return;
-        for (hipStream_t st : streams) (void)hipStreamSynchronize(st);
-        for (uintptr_t r : regs) (void)hipHostUnregister((void*)r);
-    }
-};
-
 }  // namespace
 
 const char* last_error_string() { return t_last_error.c_str(); }
@@ -550,14 +500,14 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
             if (upload[id]) memcpy(c.pinned + (size_t)slot[id] * pitch, blocks[id], (size_t)B);
         if (n_up > 0) ECG_HIP(hipMemcpyAsync(c.scratch, c.pinned, pitch * n_up, hipMemcpyHostToDevice, st));
     }
-    // large blocks: pin the caller's buffers for this call (DMA straight from them), one copy per run of
-    // blocks that are contiguous both in host memory and in the device scratch
-    std::unique_ptr<PinnedCall> pins;
+    // large blocks: pageable copies, one per run of blocks that are contiguous both in host memory and in
+    // the device scratch (the proxy's k slices of one value buffer, proxy.cpp:337-339, move as ONE copy:
+    // a single large pageable copy runs at the pinned rate, per-block 1 MiB copies at half of it).
+    // The caller's pages are deliberately NOT registered (hipHostRegister) for the call: the runtime
+    // then treats every copy that touches those pages as pinned -- including other threads' copies of
+    // neighbouring heap objects -- and unregistering under such a copy faulted the GPU
+    // (tests/test_gpu_stress.py).
     if (!staged) {
-        std::vector<std::pair<uintptr_t, uintptr_t>> spans;
-        for (int id = 0; id < nblocks; id++)
-            if (upload[id] || written[id]) spans.push_back({(uintptr_t)blocks[id], (uintptr_t)blocks[id] + (uintptr_t)B});
-        pins.reset(new PinnedCall({st}, std::move(spans)));
         int id = 0;
         while (id < nblocks) {
             if (!upload[id]) {
@@ -709,25 +659,6 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
         c.pslot_cap = 0;
         ECG_HIP(hipMalloc(&c.pslot, 3 * (slot_in + slot_out)));
         c.pslot_cap = 3 * (slot_in + slot_out);
-    }
-    // pageable batches: pin the caller's input and output regions for the call (direct DMA)
-    std::unique_ptr<PinnedCall> pins;
-    {
-        auto span = [&](const void* base, long long ss, long long bs, const std::vector<int>& ids) {
-            long long lo = 0, hi = 0;
-            bool first = true;
-            for (int id : ids) {
-                const long long o = (long long)id * bs;
-                const long long a0 = std::min(o, o + (S - 1) * ss), a1 = std::max(o, o + (S - 1) * ss) + B;
-                lo = first ? a0 : std::min(lo, a0);
-                hi = first ? a1 : std::max(hi, a1);
-                first = false;
-            }
-            return std::make_pair((uintptr_t)base + (uintptr_t)lo, (uintptr_t)base + (uintptr_t)hi);
-        };
-        pins.reset(new PinnedCall({c.pstream[0], c.pstream[1], c.pstream[2]},
-                                  {span(h_in, in_sstride, in_bstride, prog.src_ids),
-                                   span(h_out, out_sstride, out_bstride, prog.dst_ids)}));
     }
     // the device program reads compact slot blocks 0..kin-1 and writes 0..mout-1
     LinearOp dev = prog;

@@ -1,0 +1,94 @@
+"""Concurrency soak of the engine's shared state (GPU): the proxy issues EC calls from detached threads
+(proxy.cpp:416-419), so every tier must stay exact when calls from several threads interleave.
+
+Eight threads issue 400 random operations each, at once.  Each operation is one of:
+- host-tier encode / decode / partial decode of a random code family, with small (staged, zero-copy)
+  and large (pageable-copy) blocks;
+- device-tier encode on HBM blocks, sometimes inside a deferred-batch scope.
+
+The coefficient-program cache is shrunk to 8 entries, so programs are evicted while other threads'
+launches may still use them.  Every result is compared with the oracle.  This test caught a GPU fault in
+an earlier design that registered the caller's pages for large host calls (see engine.cpp run_host).
+"""
+import random
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FAMILIES = [(0, dict(k=10, m=4)), (0, dict(k=6, m=3)), (1, dict(k=4, m=2, x=2, seri_num=1)),
+            (2, dict(k=12, l=2, g=2)), (3, dict(k=8, l=3, g=2)), (4, dict(k=8, l=2, g=2)),
+            (5, dict(k=8, l=2, g=2)), (6, dict(k=8, l=2, g=2)), (7, dict(k1=4, m1=1, k2=4, m2=1)),
+            (9, dict(k1=4, m1=2, k2=2, m2=1))]
+
+
+def _worker(tid, ecg, torch, n_ops, errors):
+    from oracle import ec_ref as E
+    rng = random.Random(1000 + tid)
+    try:
+        for op in range(n_ops):
+            t, params = FAMILIES[rng.randrange(len(FAMILIES))]
+            o = E.ec_factory(t, E.CodingParameters(**params))
+            p = ecg.ec_factory(t, ecg.CodingParameters(**params))
+            k, m = o.k, o.m
+            B = rng.choice([64, 1000, 4096, 300 * 1024])  # 300 KiB: the pinned large-block path
+            data = [np.random.default_rng(tid * 100000 + op * 16 + j).integers(0, 256, B, dtype=np.uint8)
+                    for j in range(k)]
+            ref = E.zeros(m, B)
+            o.encode(data, ref, B)
+            kind = rng.randrange(4)
+            if kind == 0:  # host encode
+                got = [np.full(B, 0x33, np.uint8) for _ in range(m)]
+                assert p.encode(data, got, B) == 0
+                assert all(np.array_equal(a, b) for a, b in zip(got, ref)), ("host encode", t, params, B)
+            elif kind == 1:  # host decode of one lost block
+                stripe = [x.copy() for x in data] + [x.copy() for x in ref]
+                e = rng.randrange(k + m)
+                stripe[e][:] = 0
+                a = [x.copy() for x in stripe]
+                ra = o.decode(a[:k], a[k:], B, [e, -1], 1)
+                rb = p.decode(stripe[:k], stripe[k:], B, [e, -1], 1)
+                assert (ra == 0) == (rb == 0)
+                assert all(np.array_equal(x, y) for x, y in zip(a, stripe)), ("host decode", t, params, e)
+            elif kind == 2:  # device encode, alone or inside a deferred-batch scope
+                d = torch.from_numpy(np.stack(data + ref)).cuda()
+                d[k:] = 0
+                if rng.random() < 0.5:
+                    with ecg.batch():
+                        p.encode([d[j] for j in range(k)], [d[k + i] for i in range(m)], B)
+                else:
+                    p.encode([d[j] for j in range(k)], [d[k + i] for i in range(m)], B)
+                torch.cuda.current_stream().synchronize()
+                h = d.cpu().numpy()
+                assert all(np.array_equal(h[k + i], ref[i]) for i in range(m)), ("device encode", t, params, B)
+            else:  # host partial encode over a random data subset == XOR-able share of the parities
+                if t >= 7:
+                    continue
+                npar = o.g if hasattr(o, "g") else m
+                par = list(range(k, k + npar))
+                sub = sorted(rng.sample(range(k), rng.randint(1, k)))
+                a, b = E.zeros(npar, B), E.zeros(npar, B)
+                o.encode_partial_blocks_for_encoding([data[i] for i in sub], a, B, sub, par)
+                assert p.encode_partial_blocks_for_encoding([data[i] for i in sub], b, B, sub, par) == 0
+                assert all(np.array_equal(x, y) for x, y in zip(a, b)), ("partial", t, params, sub)
+    except Exception as e:  # noqa: BLE001
+        errors.append((tid, repr(e)))
+
+
+def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("needs an MI355X")
+    saved = ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE)
+    errors = []
+    try:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 8)
+        th = [threading.Thread(target=_worker, args=(t, ecg, torch, 400, errors)) for t in range(8)]
+        [x.start() for x in th]
+        [x.join(timeout=100) for x in th]
+        assert not any(x.is_alive() for x in th), "a worker hung"
+    finally:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
+    assert not errors, errors[:5]
