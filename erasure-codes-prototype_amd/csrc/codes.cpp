@@ -228,14 +228,7 @@ static bool ids_in_range(const std::vector<int>& v, int n) {
 
 // ================================================================================== RS / ERS
 
-const std::vector<int>& RSCode::vandermonde() {
-    if (vand_k_ != k || vand_m_ != m) {
-        vand_ = reed_sol_vandermonde_coding_matrix(k, m);
-        vand_k_ = k;
-        vand_m_ = m;
-    }
-    return vand_;
-}
+const std::vector<int>& RSCode::vandermonde() { return cached_vandermonde(k, m); }
 
 int RSCode::make_encoding_matrix(int* final_matrix) {  // rs.cpp:5-18
     const std::vector<int>& v = vandermonde();
@@ -314,7 +307,7 @@ void EnlargedRSCode::init_coding_parameters(const CodingParameters& cp) {  // rs
 
 int EnlargedRSCode::make_encoding_matrix(int* final_matrix) {  // rs.cpp:290-305
     if (seri_num >= x) return ECG_OK;  // "Invalid argurments!": the caller's zeros stay
-    std::vector<int> big = reed_sol_vandermonde_coding_matrix(x * k, m);
+    const std::vector<int>& big = cached_vandermonde(x * k, m);
     if (big.empty()) return ECG_EINVAL;
     for (int i = 0; i < m; i++)
         memcpy(&final_matrix[(size_t)i * k], &big[(size_t)i * k * x + (size_t)seri_num * k], (size_t)k * sizeof(int));
@@ -453,7 +446,7 @@ int LocallyRepairableCode::check_if_decodable(const std::vector<int>&) { return 
 
 // ---- Azure LRC (lrc.cpp:576-880)
 int Azu_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:622-644
-    std::vector<int> G = reed_sol_vandermonde_coding_matrix(k, g);
+    const std::vector<int>& G = cached_vandermonde(k, g);
     if (G.empty()) return ECG_EINVAL;
     std::fill(M, M + (size_t)k * (g + l), 0);
     std::copy(G.begin(), G.end(), M);
@@ -534,7 +527,7 @@ static std::vector<int> mix_local(const std::vector<int>& L, const std::vector<i
 
 // ---- Azure LRC + 1 (lrc.cpp:881-1094)
 int Azu_LRC_1::make_encoding_matrix(int* M) {  // lrc.cpp:933-981
-    std::vector<int> G = reed_sol_vandermonde_coding_matrix(k, g);
+    const std::vector<int>& G = cached_vandermonde(k, g);
     if (G.empty() || l < 1) return ECG_EINVAL;
     std::fill(M, M + (size_t)k * (g + l), 0);
     std::copy(G.begin(), G.end(), M);
@@ -588,7 +581,7 @@ std::string Azu_LRC_1::self_information() const {
 
 // ---- Optimal LRC (lrc.cpp:1096-1307)
 int Opt_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:1168-1215
-    std::vector<int> G = reed_sol_vandermonde_coding_matrix(k, g);
+    const std::vector<int>& G = cached_vandermonde(k, g);
     if (G.empty()) return ECG_EINVAL;
     std::fill(M, M + (size_t)k * (g + l), 0);
     std::copy(G.begin(), G.end(), M);
@@ -629,7 +622,7 @@ std::string Opt_LRC::self_information() const {
 
 // ---- Optimal Cauchy LRC (lrc.cpp:1309-1755)
 int Opt_Cau_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:1485-1518
-    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    const std::vector<int>& C = cached_cauchy_good(k, g + 1);
     if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
     std::fill(M, M + (size_t)k * (g + l), 0);
     std::copy(C.begin(), C.begin() + (size_t)g * k, M);
@@ -644,7 +637,7 @@ int Opt_Cau_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:1485-1518
 }
 
 int Opt_Cau_LRC::make_group_matrix(int* gm, int group_id, int size) {  // lrc.cpp:1574-1591
-    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    const std::vector<int>& C = cached_cauchy_good(k, g + 1);
     if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
     int idx = 0;
     for (int i = 0; i < l; i++) {
@@ -692,7 +685,7 @@ std::string Opt_Cau_LRC::self_information() const {
 
 // ---- Uniform Cauchy LRC (lrc.cpp:2025-2310)
 int Uni_Cau_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:2097-2156
-    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    const std::vector<int>& C = cached_cauchy_good(k, g + 1);
     if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
     std::fill(M, M + (size_t)k * (g + l), 0);
     std::copy(C.begin(), C.begin() + (size_t)g * k, M);
@@ -715,7 +708,7 @@ int Uni_Cau_LRC::make_encoding_matrix(int* M) {  // lrc.cpp:2097-2156
 }
 
 int Uni_Cau_LRC::make_group_matrix(int* gm, int group_id, int size) {  // lrc.cpp:2213-2230
-    std::vector<int> C = cauchy_good_general_coding_matrix(k, g + 1);
+    const std::vector<int>& C = cached_cauchy_good(k, g + 1);
     if (C.empty()) return g + 1 == 2 ? ECG_EUNPINNED : ECG_EINVAL;
     int idx = 0;
     for (int i = 0; i < l; i++) {

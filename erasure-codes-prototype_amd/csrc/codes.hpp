@@ -7,7 +7,9 @@
 // Differences from the reference, all deliberate:
 //   * methods return int status instead of void (the reference prints and returns);
 //   * blocks may be host (reference semantics) or device pointers (`mem`, `stream`);
-//   * coding matrices are cached per object instead of rebuilt per call (rs.cpp:22-23).
+//   * coding matrices come from a process-wide (k, m) cache instead of being rebuilt per call
+//     (rs.cpp:22-23); the objects keep no lazily-filled state, so concurrent calls on one object are
+//     safe as long as its parameters are not changed meanwhile.
 // Partitioning (placement of a stripe's blocks over clusters) and repair planning (which helper blocks each
 // cluster contributes to a partial-decoding repair) are host logic in planning.cpp.
 #pragma once
@@ -168,9 +170,7 @@ public:
     std::vector<int> full_matrix();  // [I_k ; M]
 
 protected:
-    const std::vector<int>& vandermonde();  // reed_sol_vandermonde_coding_matrix(k, m), cached
-    std::vector<int> vand_;
-    int vand_k_ = -1, vand_m_ = -1;
+    const std::vector<int>& vandermonde();  // reed_sol_vandermonde_coding_matrix(k, m), cached process-wide
 };
 
 class EnlargedRSCode : public RSCode {

@@ -3,6 +3,9 @@
 
 #include <algorithm>
 
+#include <map>
+#include <mutex>
+
 #include "gf256.hpp"
 
 namespace ecg {
@@ -121,6 +124,25 @@ void cauchy_improve_coding_matrix(int k, int m, std::vector<int>& M) {
             for (int j = 0; j < k; j++) row[j] = gf::mul(row[j], s);
         }
     }
+}
+
+namespace {
+std::mutex g_builder_mu;
+std::map<std::pair<int, int>, std::vector<int>> g_vand, g_cauchy;
+}  // namespace
+
+const std::vector<int>& cached_vandermonde(int k, int m) {
+    std::lock_guard<std::mutex> lk(g_builder_mu);
+    auto it = g_vand.find({k, m});
+    if (it == g_vand.end()) it = g_vand.emplace(std::make_pair(k, m), reed_sol_vandermonde_coding_matrix(k, m)).first;
+    return it->second;
+}
+
+const std::vector<int>& cached_cauchy_good(int k, int m) {
+    std::lock_guard<std::mutex> lk(g_builder_mu);
+    auto it = g_cauchy.find({k, m});
+    if (it == g_cauchy.end()) it = g_cauchy.emplace(std::make_pair(k, m), cauchy_good_general_coding_matrix(k, m)).first;
+    return it->second;
 }
 
 std::vector<int> cauchy_good_general_coding_matrix(int k, int m) {

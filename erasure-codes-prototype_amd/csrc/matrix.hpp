@@ -14,6 +14,11 @@ std::vector<int> reed_sol_vandermonde_coding_matrix(int k, int m);
 // cauchy_good_general_coding_matrix(k, m, 8).  m == 2 selects Jerasure's hard-coded cbest_8 table,
 // which is not available offline: returns empty (status ECG_EUNPINNED at the C ABI).
 std::vector<int> cauchy_good_general_coding_matrix(int k, int m);
+// The same two builders through a process-wide, mutex-protected cache keyed by (k, m): the facade's
+// objects call them per operation (the reference rebuilds them per call, rs.cpp:22-23, lrc.cpp:27);
+// entries are never dropped (at most one per distinct (k, m)), so the references stay valid.
+const std::vector<int>& cached_vandermonde(int k, int m);
+const std::vector<int>& cached_cauchy_good(int k, int m);
 std::vector<int> cauchy_original_coding_matrix(int k, int m);
 void cauchy_improve_coding_matrix(int k, int m, std::vector<int>& M);
 int cauchy_n_ones(int e);
