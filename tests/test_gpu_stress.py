@@ -10,6 +10,7 @@ The coefficient-program cache is shrunk to 8 entries, so programs are evicted wh
 launches may still use them.  Every result is compared with the oracle.  This test caught a GPU fault in
 an earlier design that registered the caller's pages for large host calls (see engine.cpp run_host).
 """
+import os
 import random
 import threading
 
@@ -85,9 +86,10 @@ def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle):
     errors = []
     try:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 8)
-        th = [threading.Thread(target=_worker, args=(t, ecg, torch, 400, errors)) for t in range(8)]
+        n_ops = int(os.environ.get("ECG_SOAK_OPS", "400"))  # longer soaks: ECG_SOAK_OPS=2000
+        th = [threading.Thread(target=_worker, args=(t, ecg, torch, n_ops, errors)) for t in range(8)]
         [x.start() for x in th]
-        [x.join(timeout=100) for x in th]
+        [x.join(timeout=100 + n_ops // 10) for x in th]
         assert not any(x.is_alive() for x in th), "a worker hung"
     finally:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
