@@ -283,6 +283,42 @@ int ecg_decode_batch_host(int k, int m, const int* matrix, int row_k_ones, const
                                                 chunk_stripes);
 }
 
+int ecg_make_decode_matrix(int k, int m, const int* matrix, int row_k_ones, const int* erasures, int* src_ids,
+                           int cap_src, int* n_src, int* dst_ids, int cap_dst, int* n_dst, int* coef) {
+    if (k < 1 || m < 1 || !matrix || !erasures || !n_src || !n_dst) return ECG_EINVAL;
+    std::vector<LinearOp> ops;
+    if (plan_matrix_decode(k, m, matrix, row_k_ones, erasures, ops) < 0) return ECG_EUNDECODABLE;
+    if (ops.size() > 1) return ECG_EINVAL;
+    const LinearOp empty;
+    const LinearOp& op = ops.empty() ? empty : ops[0];
+    *n_src = op.k_in();
+    *n_dst = op.m_out();
+    if (cap_src >= op.k_in() && cap_dst >= op.m_out() && src_ids && dst_ids && coef) {
+        std::copy(op.src_ids.begin(), op.src_ids.end(), src_ids);
+        std::copy(op.dst_ids.begin(), op.dst_ids.end(), dst_ids);
+        for (size_t i = 0; i < op.coef.size(); i++) coef[i] = op.coef[i];
+    }
+    return ECG_OK;
+}
+
+int ecg_region_xor_batch(const void* d_src, long long src_stride, void* d_dst, long long dst_stride,
+                         long long nbytes, int S, void* stream) {
+    if (S < 0 || nbytes < 0) return ECG_EINVAL;
+    if (S == 0 || nbytes == 0) return ECG_OK;
+    if (!d_src || !d_dst) return ECG_EINVAL;
+    LinearOp op;
+    op.src_ids = {0, 1};
+    op.dst_ids = {1};
+    op.coef = {1, 1};
+    std::vector<std::vector<const uint8_t*>> blk((size_t)S);
+    std::vector<const uint8_t* const*> calls((size_t)S);
+    for (int s = 0; s < S; s++) {
+        blk[s] = {(const uint8_t*)d_src + (size_t)s * src_stride, (const uint8_t*)d_dst + (size_t)s * dst_stride};
+        calls[s] = blk[s].data();
+    }
+    return Engine::instance().run_ptr_batch(op, calls, nbytes, (hipStream_t)stream);
+}
+
 int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, long long in_sstride,
                                long long in_bstride, void* d_out, long long out_sstride, long long out_bstride,
                                long long B, int S, void* stream) {

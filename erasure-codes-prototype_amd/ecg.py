@@ -66,7 +66,7 @@ EXPORTS = [
     "ecg_batch_begin", "ecg_batch_flush", "ecg_batch_end",
     "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
     "ecg_encode_batch",
-    "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
+    "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_make_decode_matrix", "ecg_region_xor_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
     "ecg_fill_random",
     "ecg_ec_factory", "ecg_ec_destroy", "ecg_ec_init_coding_parameters", "ecg_ec_get_coding_parameters",
     "ecg_ec_set_memory", "ecg_ec_set_isvertical", "ecg_ec_k", "ecg_ec_m", "ecg_ec_make_encoding_matrix",
@@ -144,6 +144,8 @@ def lib():
     sig = {
         "ecg_last_error": ([], ctypes.c_char_p),
         "ecg_version": ([], I),
+        "ecg_make_decode_matrix": ([I, I, IP, I, IP, IP, I, IP, IP, I, IP, IP], I),
+        "ecg_region_xor_batch": ([P, LL, P, LL, LL, I, P], I),
         "ecg_program_cache_size": ([], I),
         "ecg_batch_begin": ([], I),
         "ecg_batch_flush": ([], I),
@@ -409,6 +411,26 @@ def matrix_apply_batch_multi(programs, d_in, d_out, prog_of_stripe=None, stripe_
         prog_of_stripe.data_ptr() if prog_of_stripe is not None else None,
         stripe_of.data_ptr() if stripe_of is not None else None,
         d_in.data_ptr(), iss, ibs, d_out.data_ptr(), oss, obs, B, S, _stream(stream)), "matrix_apply_batch_multi")
+
+
+def make_decode_matrix(k, m, matrix, row_k_ones, erasures):
+    """jerasure_matrix_decode composed into one map: (src_ids, dst_ids, coef[n_dst][n_src]) or raises."""
+    n_src, n_dst = ctypes.c_int(0), ctypes.c_int(0)
+    er = _ints(list(erasures) + ([-1] if not erasures or erasures[-1] != -1 else []))
+    _check(lib().ecg_make_decode_matrix(k, m, _ints(matrix), int(bool(row_k_ones)), er, None, 0, ctypes.byref(n_src),
+                                        None, 0, ctypes.byref(n_dst), None), "make_decode_matrix")
+    ns, nd = n_src.value, n_dst.value
+    src, dst, coef = (ctypes.c_int * max(1, ns))(), (ctypes.c_int * max(1, nd))(), (ctypes.c_int * max(1, ns * nd))()
+    _check(lib().ecg_make_decode_matrix(k, m, _ints(matrix), int(bool(row_k_ones)), er, src, ns, ctypes.byref(n_src),
+                                        dst, nd, ctypes.byref(n_dst), coef), "make_decode_matrix")
+    return list(src)[:ns], list(dst)[:nd], [list(coef)[i * ns:(i + 1) * ns] for i in range(nd)]
+
+
+def region_xor_batch(d_src, d_dst, stream=None):
+    """dst[s] ^= src[s] for every row s of two [S][nbytes] uint8 CUDA tensors (galois_region_xor, batched)."""
+    S, n = d_src.shape
+    return _check(lib().ecg_region_xor_batch(d_src.data_ptr(), d_src.stride(0), d_dst.data_ptr(), d_dst.stride(0), n, S,
+                                             _stream(stream)), "region_xor_batch")
 
 
 def perform_addition_batch(block_num, parity_num, d_in, d_out, stream=None):

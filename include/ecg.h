@@ -86,6 +86,16 @@ int ecg_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int
 int ecg_jerasure_matrix_decode(int k, int m, int w, int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
                                char** coding_ptrs, int size);
 
+/* Host-side decode planning (SURVEY.md §8(b) "ecg_make_decode_matrix"): the whole of
+ * jerasure_matrix_decode(k, m, matrix, row_k_ones, erasures) composed into ONE linear map.  Written
+ * block dst_ids[i] = XOR_j coef[i * n_src + j] * block src_ids[j], block ids data 0..k-1 and coding
+ * k..k+m-1, destinations in the library's write order.  Returns 0 with *n_src / *n_dst set (the arrays
+ * are written only when cap_src >= *n_src and cap_dst >= *n_dst; coef needs *n_dst * *n_src ints),
+ * ECG_EUNDECODABLE where the library returns -1, or ECG_EINVAL (bad arguments, or a pattern whose
+ * library order reads a block after writing it, which has no single-map form). */
+int ecg_make_decode_matrix(int k, int m, const int* matrix, int row_k_ones, const int* erasures, int* src_ids,
+                           int cap_src, int* n_src, int* dst_ids, int cap_dst, int* n_dst, int* coef);
+
 /* ---------------------------------------------------------------- tier 2: device / batched
  * All pointers below are DEVICE pointers; `stream` is a hipStream_t (NULL = default stream);
  * calls are asynchronous.  Block pointers must be 16-byte aligned for the vector path (otherwise a
@@ -132,6 +142,10 @@ int ecg_encode_batch(int k, int m, const int* matrix, const void* d_in, long lon
 int ecg_decode_batch(int k, int m, const int* matrix, int row_k_ones, const int* patterns, int n_patterns,
                      const int* d_pattern_of_stripe, void* d_stripes, long long sstride, long long bstride,
                      void* d_out, long long out_sstride, long long out_bstride, long long B, int S, void* stream);
+/* Batched galois_region_xor: dst_s ^= src_s for S regions of nbytes (DEVICE pointers), region s at
+ * d_src + s * src_stride and d_dst + s * dst_stride. */
+int ecg_region_xor_batch(const void* d_src, long long src_stride, void* d_dst, long long dst_stride,
+                         long long nbytes, int S, void* stream);
 /* Batched perform_addition (erasure_code.cpp:70-94): parity i of stripe s = XOR_j partial[j*parity_num+i]. */
 int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, long long in_sstride,
                                long long in_bstride, void* d_out, long long out_sstride, long long out_bstride,

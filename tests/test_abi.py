@@ -212,3 +212,34 @@ def test_tuning_options_validation(ecg):
             ecg.set_option(o, v)
     if "ECG_GRID_MAP" not in os.environ:
         assert saved[ecg.ECG_OPT_GRID_MAP] == 3  # auto
+
+
+@pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])
+def test_make_decode_matrix_equals_library_decode(ecg, oracle, k, m, row_k_ones):
+    """ecg_make_decode_matrix (host only, no GPU): the composed map, applied with the oracle's own
+    matrix product to the blocks it names, rebuilds exactly what the oracle's jerasure_matrix_decode
+    writes, in the library's write order; > m erasures is ECG_EUNDECODABLE like the library's -1."""
+    import numpy as np
+    rng = random.Random(k * 10 + m + row_k_ones)
+    B = 96
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    data = [np.frombuffer(rng.randbytes(B), dtype=np.uint8).copy() for _ in range(k)]
+    coding = [np.zeros(B, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, data, coding, B)
+    stripe = data + coding
+    for _ in range(25):
+        pat = rng.sample(range(k + m), rng.randint(1, m))
+        src, dst, coef = ecg.make_decode_matrix(k, m, M, row_k_ones, pat)
+        assert sorted(dst) == sorted(pat) and not set(src) & set(pat)
+        out = [np.zeros(B, np.uint8) for _ in dst]
+        oracle.jerasure_matrix_encode(len(src), len(dst), [c for row in coef for c in row], [stripe[i] for i in src],
+                                      out, B)
+        lost = [x.copy() for x in stripe]
+        for i in pat:
+            lost[i][:] = 0
+        assert oracle.jerasure_matrix_decode(k, m, M, row_k_ones, pat + [-1], lost[:k], lost[k:], B) == 0
+        for i, d in enumerate(dst):
+            assert np.array_equal(out[i], lost[d]), (pat, d)
+    with pytest.raises(ecg.EcgError) as e:
+        ecg.make_decode_matrix(k, m, M, row_k_ones, list(range(m + 1)))
+    assert e.value.code == ecg.ECG_EUNDECODABLE

@@ -1001,3 +1001,19 @@ def test_large_host_blocks_pinned_for_the_call(ecg, oracle, torch_cuda):
     stripe[k + 1][:] = 0xEE
     assert ecg.jerasure_matrix_decode(k, m, M, 2, [3, k + 1, -1], stripe[:k], stripe[k:], B) == 0
     assert np.array_equal(stripe[3], lost[0]) and np.array_equal(stripe[k + 1], lost[1])
+
+
+def test_region_xor_batch(ecg, oracle, torch_cuda):
+    """ecg_region_xor_batch: galois_region_xor (dst ^= src) over S regions, any strides / sizes."""
+    torch = torch_cuda
+    for S, n in [(1, 1), (7, 1000), (64, 4096 + 3), (3, 1 << 20)]:
+        src = torch.randint(0, 256, (S, n + 16), dtype=torch.uint8, device="cuda")[:, 5:5 + n]  # odd stride/offset
+        dst = torch.randint(0, 256, (S, n), dtype=torch.uint8, device="cuda")
+        expect = (src.cpu().numpy() ^ dst.cpu().numpy())
+        ecg.region_xor_batch(src, dst)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst.cpu().numpy(), expect), (S, n)
+        a, b = np.frombuffer(bytes(src[0].cpu().numpy()), np.uint8).copy(), dst[0].cpu().numpy().copy()
+        c = b.copy()
+        oracle.galois_region_xor(a, c, n)  # self-inverse: XOR the source back in
+        assert np.array_equal(c, b ^ a)
