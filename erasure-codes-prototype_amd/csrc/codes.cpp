@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <typeinfo>
 
 #include "engine.hpp"
 #include "gf256.hpp"
@@ -112,17 +113,43 @@ void ErasureCode::partial_decoding_matrix_(int k_, const int* full, const std::v
 int ErasureCode::run(const Plan& plan, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding,
                      long long B) {
     if (plan.ops.empty()) return ECG_OK;
-    std::vector<uint8_t*> blocks((size_t)n_data + n_coding, nullptr);
+    const int n = n_data + n_coding;
+    uint8_t* small[64];  // the common case needs no allocation (per-stripe calls are launch-rate bound)
+    std::vector<uint8_t*> large;
+    uint8_t** blocks = small;
+    if (n > 64) {
+        large.resize((size_t)n);
+        blocks = large.data();
+    }
     for (int i = 0; i < n_data; i++) blocks[i] = (uint8_t*)data_ptrs[i];
-    for (int i = 0; i < n_coding; i++) blocks[(size_t)n_data + i] = (uint8_t*)coding_ptrs[i];
+    for (int i = 0; i < n_coding; i++) blocks[n_data + i] = (uint8_t*)coding_ptrs[i];
     Engine& eng = Engine::instance();
-    if (mem == ECG_MEM_DEVICE) return eng.run_device(plan.ops, blocks.data(), (int)blocks.size(), B, stream);
-    return eng.run_host(plan.ops, blocks.data(), (int)blocks.size(), B);
+    if (mem == ECG_MEM_DEVICE) return eng.run_device(plan.ops, blocks, n, B, stream);
+    return eng.run_host(plan.ops, blocks, n, B);
 }
 
-int ErasureCode::run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B) {
+int ErasureCode::run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B,
+                            bool stable_matrix) {
+    // The encode plan's block ids are already the call's (data 0..kk-1, coding kk..kk+mm-1).  A matrix
+    // from the process-wide builder cache never changes behind its pointer, so its plan is reused
+    // (one entry per thread): the per-stripe call then allocates nothing for planning.
+    if (stable_matrix) {
+        thread_local const int* last_matrix = nullptr;
+        thread_local int last_k = -1, last_m = -1;
+        thread_local Plan last_plan;
+        if (matrix != last_matrix || kk != last_k || mm != last_m) {
+            last_plan.ops.clear();
+            LinearOp op = plan_matrix_encode(kk, mm, matrix);
+            if (op.m_out() > 0) last_plan.ops.push_back(std::move(op));
+            last_matrix = matrix;
+            last_k = kk;
+            last_m = mm;
+        }
+        return run(last_plan, data_ptrs, kk, coding_ptrs, mm, B);
+    }
     Plan p;
-    append_encode(p, kk, mm, matrix, iota_ids(kk), iota_ids(mm, kk));
+    LinearOp op = plan_matrix_encode(kk, mm, matrix);
+    if (op.m_out() > 0) p.ops.push_back(std::move(op));
     return run(p, data_ptrs, kk, coding_ptrs, mm, B);
 }
 
@@ -245,10 +272,15 @@ std::vector<int> RSCode::full_matrix() {  // rs.cpp:48-50
 }
 
 int RSCode::encode(char** data_ptrs, char** coding_ptrs, int block_size) {  // rs.cpp:20-25
-    std::vector<int> M((size_t)k * m, 0);
-    int rc = make_encoding_matrix(M.data());
-    if (rc != ECG_OK) return rc;
-    return run_encode(k, m, M.data(), data_ptrs, coding_ptrs, block_size);
+    if (typeid(*this) != typeid(RSCode)) {  // EnlargedRSCode: its own make_encoding_matrix
+        std::vector<int> M((size_t)k * m, 0);
+        int rc = make_encoding_matrix(M.data());
+        if (rc != ECG_OK) return rc;
+        return run_encode(k, m, M.data(), data_ptrs, coding_ptrs, block_size);
+    }
+    const std::vector<int>& v = vandermonde();
+    if (v.empty()) return ECG_EINVAL;
+    return run_encode(k, m, v.data(), data_ptrs, coding_ptrs, block_size, /*stable_matrix=*/true);
 }
 
 // rs.cpp:27-42.  NB: decodes with reed_sol_vandermonde_coding_matrix(k, m) even for EnlargedRSCode,

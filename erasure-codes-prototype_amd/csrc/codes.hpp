@@ -134,7 +134,8 @@ protected:
     // Execute a plan over data_ptrs (n_data) ++ coding_ptrs (n_coding) on this object's memory tier.
     int run(const Plan& plan, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding, long long B);
     // jerasure_matrix_encode / _decode over this call's pointers
-    int run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B);
+    int run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B,
+                   bool stable_matrix = false);
     int run_with_addition(const std::vector<int>& R, int nl, int nf, char** local_ptrs, char** partial_ptrs,
                           int n_partials, char** out_ptrs, long long B);
     int run_decode(int kk, int mm, const int* matrix, int row_k_ones, int* erasures, char** data_ptrs,

@@ -221,6 +221,9 @@ bool op_is_binary(const LinearOp& op) {
 
 LinearOp plan_matrix_encode(int k, int m, const int* matrix) {
     LinearOp op;
+    op.src_ids.reserve(k);
+    op.dst_ids.reserve(m);
+    op.coef.reserve((size_t)k * m);
     for (int j = 0; j < k; j++) op.src_ids.push_back(j);
     for (int i = 0; i < m; i++) {
         const int* row = matrix + (size_t)i * k;
