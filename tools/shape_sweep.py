@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--maps", default="1,2")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--shapes", default="grid", choices=["grid", "baseline"],
+                    help="grid: k_in x m_out in {1,4,10} x {1,2,4}; baseline: the shapes the BASELINE workloads run")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     S, B, n = a.stripes, a.block, 14
@@ -35,11 +37,17 @@ def main():
     sep = torch.empty((S, 4, B), dtype=torch.uint8, device="cuda")
     rng = np.random.default_rng(1)
     variants = []
-    for k_in in (1, 4, 10):
-        for m_out in (1, 2, 4):
+    if a.shapes == "grid":
+        shapes = [(k, mm, w) for k in (1, 4, 10) for mm in (1, 2, 4) for w in ("in-stripe", "separate")]
+    else:  # RS(10,4) encode / decodes, Azure(12,2,2) encode + local/global repair, PC row merge, partials
+        shapes = [(10, 4, "in-stripe"), (10, 1, "separate"), (10, 2, "separate"), (10, 4, "separate"),
+                  (12, 2, "in-stripe"), (6, 1, "separate"), (12, 1, "separate"), (8, 1, "separate"),
+                  (3, 1, "separate"), (4, 1, "separate")]
+    for k_in, m_out, where_only in shapes:
+        if True:
             coef = rng.integers(2, 256, size=(m_out, k_in))
             src = list(range(k_in))
-            for where in ("in-stripe", "separate"):
+            for where in (where_only,):
                 if where == "in-stripe":
                     dst, out = list(range(k_in, k_in + m_out)), stripes
                 else:
