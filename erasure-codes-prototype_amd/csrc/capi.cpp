@@ -44,7 +44,7 @@ int emit(const std::vector<int>& v, int* buf, int cap) {
 extern "C" {
 
 const char* ecg_last_error(void) { return last_error_string(); }
-int ecg_version(void) { return 100; }
+int ecg_version(void) { return 101; }  // 1.1: batch scope, fused repair/merge calls, decode-matrix export
 
 int ecg_device_count(void) {
     int n = 0;
