@@ -14,6 +14,8 @@ Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line
   lrc-repair  configs[2]: Azure-LRC(12,2,2), 1 MiB, single-block repair of block s mod 16 of every
               stripe, partial_decoding=true (helper partials + main partial + perform_addition) and the
               fused single-launch form;
+  lrc-repair-ring  configs[2]'s partial decoding with helper and main proxies on neighbouring GPUs:
+              helper partials sent over xGMI (RCCL point to point), added in the main rank's fused kernel;
   pc-merge    configs[3]: PC(4,1,4,1), 4 MiB blocks, stripe merging x=2 (HORIZONTAL): the 5 row
               parities of the merged PC(8,1,4,1) recomputed from the two old stripes;
   rs4m-waves  configs[4]: RS(10,4), 4 MiB blocks, 65536 stripes split over the ranks, encoded in
@@ -51,10 +53,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs-encode-decode",
-                    choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "pc-merge", "rs4m-waves",
-                             "rs-host"])
+                    choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "lrc-repair-ring", "pc-merge",
+                             "rs4m-waves", "rs-host"])
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
+    ap.add_argument("--chunk", type=int, default=None, help="lrc-repair-ring: stripes per transfer")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
@@ -246,6 +249,35 @@ def rs_decode_patterns(a, r):
 
 # ------------------------------------------------------------------------------- config 3
 
+AZURE_OPTIMAL_PARTS = [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9, 10, 11], [14, 15, 12, 13]]
+
+
+def azure_local_split(e, k=12, parts=AZURE_OPTIMAL_PARTS):
+    """Azure-LRC(12,2,2) local repair of block e (data or local parity): the 6 survivors of its group and
+    their split into [helper set, main set] under the OPTIMAL partition.  A partition
+    other than the failed block's sends one partial when it holds more than f = 1 survivors, otherwise
+    its blocks go to the main proxy directly (handle_repair.cpp:169-176); the main proxy adds its own
+    partial over its partition's survivors + the direct blocks (perform_addition,
+    handle_repair.cpp:371-376).  For every local pattern of this code that is two sets of three."""
+    gid = e // 6 if e < k else e - 14
+    group = list(range(6 * gid, 6 * gid + 6)) + [14 + gid]
+    surv = [b for b in group if b != e]
+    main_part = next(p for p in parts if e in p)
+    mine = [b for b in surv if b in main_part]
+    helpers = []
+    for p in parts:
+        if p is main_part:
+            continue
+        inside = [b for b in surv if b in p]
+        if len(inside) > 1:
+            helpers.append(inside)
+        else:
+            mine += inside
+    sets = helpers + ([mine] if mine else [])
+    assert len(sets) == 2 and all(len(x) == 3 for x in sets), (e, sets)
+    return surv, sets
+
+
 def lrc_repair(a, r):
     """Azure-LRC(12,2,2), 1 MiB: every stripe loses block e = s mod 16 and repairs it.
     Data / local-parity loss: local group of 6 survivors.  partial_decoding=true mirrors
@@ -270,35 +302,14 @@ def lrc_repair(a, r):
     rebuilt = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
     partials = torch.empty((S, 2, B), dtype=torch.uint8, device="cuda")
     e_of = torch.arange(S, device="cuda", dtype=torch.int32) % n
-    # OPTIMAL partition of Azure(12,2,2): {0,1,2},{3,4,5},{6,7,8},{9,10,11},{14,15,12,13}.
-    # A partition other than the failed block's sends one partial when it holds more than f = 1
-    # survivors, otherwise its blocks go to the main proxy directly (handle_repair.cpp:169-176); the
-    # main proxy adds its own partial over its partition's survivors + the direct blocks and XOR-sums
-    # (perform_addition, handle_repair.cpp:371-376).  For every local pattern of this code that gives
-    # exactly two partials of three survivors each.
-    parts = [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9, 10, 11], [14, 15, 12, 13]]
+    # helper / main split of every local pattern: azure_local_split
     fused_progs, part_progs, cls_local = [], ([], []), []
     helper_progs, main_progs = [], []  # fused-main form: helper partial -> slot n, main (3 + 1 inputs) -> out
     for e in range(n):
         if e in (12, 13):
             continue
-        gid = e // 6 if e < k else e - 14
-        group = list(range(6 * gid, 6 * gid + 6)) + [14 + gid]
-        surv = [b for b in group if b != e]
+        surv, sets = azure_local_split(e)
         fused_progs.append((ec.partial_decoding_matrix(surv, surv, [e]), surv, [0]))
-        main_part = next(p for p in parts if e in p)
-        mine = [b for b in surv if b in main_part]
-        helpers = []
-        for p in parts:
-            if p is main_part:
-                continue
-            inside = [b for b in surv if b in p]
-            if len(inside) > 1:
-                helpers.append(inside)
-            else:
-                mine += inside
-        sets = helpers + ([mine] if mine else [])
-        assert len(sets) == 2 and all(len(x) == 3 for x in sets), (e, sets)
         for i in range(2):
             part_progs[i].append((ec.partial_decoding_matrix(sets[i], surv, [e]), sets[i], [i]))
         helper_progs.append((ec.partial_decoding_matrix(sets[0], surv, [e]), sets[0], [n]))
@@ -366,6 +377,91 @@ def lrc_repair(a, r):
                          "executed_GBps": round(executed / t / 1e9, 1)}
     return {"workload": "Azure-LRC(12,2,2) single-block repair, block s mod 16, 1 MiB", "n_gpus": r.world,
             "stripes_per_gpu": S, "steps": a.steps, "results": results, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated on device)"}
+
+
+def ring_repair_state(r, S, B, chunk):
+    """Set-up of lrc-repair-ring (below) on rank r: returns (step, rebuilt, e_main, main_view); step()
+    runs one pipelined repair of the rank's S stripes.  tests/test_gpu_ring.py drives the same state."""
+    k, l, g = 12, 2, 2
+    n = k + g + l
+    cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
+    ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)
+    M = ec.make_encoding_matrix()
+    cls_local = [e for e in range(n) if e not in (12, 13)]
+    helper_progs, main_progs = [], []
+    for e in cls_local:
+        surv, sets = azure_local_split(e)
+        helper_progs.append((ec.partial_decoding_matrix(sets[0], surv, [e]), sets[0], [n]))
+        main_progs.append(([list(ec.partial_decoding_matrix(sets[1], surv, [e])) + [1]], sets[1] + [n], [0]))
+
+    def make_store(owner):
+        st = torch.empty((n + 1, S, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(st, 0xEC0DE, word_offset=D.data_word_offset(owner * S, n + 1, B))
+        view = st.permute(1, 0, 2)  # [S][n + 1][B], stripe stride B, block stride S * B
+        ecg.encode_batch(k, g + l, M, view[:, :k], view[:, k:n])
+        return st, view
+
+    nxt = (r.rank + 1) % r.world
+    main_store, main_view = make_store(r.rank)
+    help_store, help_view = (main_store, main_view) if r.world == 1 else make_store(nxt)
+    idx = torch.arange(S, device="cuda", dtype=torch.int32)
+    prog_main = ((idx + r.rank * S) % len(cls_local)).contiguous()
+    prog_help = ((idx + nxt * S) % len(cls_local)).contiguous()
+    e_main = torch.tensor(cls_local, device="cuda")[prog_main.long()]
+    rebuilt = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
+    send, recv = help_store[n], main_store[n]
+
+    def helper(c0, c1):
+        ecg.matrix_apply_batch_multi(helper_progs, help_view[c0:c1], help_view[c0:c1], prog_of_stripe=prog_help[c0:c1])
+
+    def main_(c0, c1):
+        ecg.matrix_apply_batch_multi(main_progs, main_view[c0:c1], rebuilt[c0:c1], prog_of_stripe=prog_main[c0:c1])
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        D.pipelined_ring_repair(S, chunk, helper, main_, send, recv, r)
+        if ev:
+            ev[1].record()
+
+    return step, rebuilt, e_main, main_view
+
+
+def lrc_repair_ring(a, r):
+    """Config 3 with the proxies on different GPUs: cross-GPU partial decoding.
+
+    Azure-LRC(12,2,2), local repairs only (block e = the (s mod 14)-th data / local-parity block of
+    stripe s).  Rank q holds S stripes as the MAIN proxy and, for the next rank's S stripes, the
+    helper partition's blocks as the HELPER proxy (every rank regenerates the owner's bytes; blocks
+    stored block-major, [n + 1][S][B], so the partial slot n of a stripe range is one contiguous
+    region).  Per chunk of stripes: the helper-partial kernel (3 survivors -> slot n), RCCL send of the
+    chunk's partials to the next rank over xGMI (ring_exchange), and the main rank's fused kernel
+    (3 own survivors + the received partial -> repaired block), pipelined so transfers run back to
+    back (ecg_dist.pipelined_ring_repair).  One rank: the partial stays in place (no exchange)."""
+    B = a.block_size or (1 << 20)
+    S = a.stripes or 1024
+    # one rank: nothing to overlap, one launch per kernel; N > 1: 128 MiB transfers
+    chunk = max(1, min(S, a.chunk or (S if r.world == 1 else 128)))
+    step, rebuilt, e_main, main_view = ring_repair_state(r, S, B, chunk)
+    rebuilt.zero_()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    lost = main_view[torch.arange(S, device="cuda"), e_main]
+    ok = bool(torch.equal(rebuilt[:, 0], lost))
+    del lost
+    assert ok, "ring repair mismatch"
+    elapsed, evs = timed_loop(r, a.steps, step)
+    t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+    return {"workload": "Azure-LRC(12,2,2) local repair, helper and main proxies on neighbouring GPUs, 1 MiB",
+            "n_gpus": r.world, "stripes_per_gpu": S, "chunk_stripes": chunk, "steps": a.steps,
+            "repairs_per_s": round(r.world * S * a.steps / elapsed, 1),
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "ms_per_step_rank0_events": round(t * 1e3, 3),
+            "xgmi_bytes_per_rank_step": S * B if r.world > 1 else 0,
+            "xgmi_GBps_per_rank": round(S * B * a.steps / elapsed / 1e9, 1) if r.world > 1 else 0.0,
+            "hbm_executed_bytes_per_rank_step": 9 * S * B, "verified": ok, "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
@@ -526,7 +622,8 @@ def main():
     else:
         D.init(r, "nccl", device=torch.device("cuda", dev) if r.distributed else None)
     ecg.lib().ecg_set_device(torch.cuda.current_device())
-    fn = {"rs-encode-decode": rs_encode_decode, "rs-decode-patterns": rs_decode_patterns, "lrc-repair": lrc_repair, "pc-merge": pc_merge,
+    fn = {"rs-encode-decode": rs_encode_decode, "rs-decode-patterns": rs_decode_patterns, "lrc-repair": lrc_repair,
+          "lrc-repair-ring": lrc_repair_ring, "pc-merge": pc_merge,
           "rs4m-waves": rs4m_waves, "rs-host": rs_host}[a.workload]
     line = fn(a, r)
     if r.rank == 0:

@@ -6,6 +6,13 @@ used only around the data path: a broadcast of the coding plan from rank 0 (codi
 patterns) before it, a barrier before/after the timed region, a MAX of elapsed times, a SUM of
 processed bytes and an all-gather of per-rank 64-bit parity checksums for a bit-exact verdict.
 Backend "nccl" (RCCL over xGMI) on GPUs, "gloo" in CPU tests.
+
+The one real exchange step is cross-GPU partial decoding ("clusters -> GPUs"): a
+helper proxy's partial block travels to the main proxy, which XOR-adds it to its own partial
+(help_repair -> main_repair, handle_repair.cpp:249-384).  RCCL has no XOR reduction, so the partials
+move point to point (`ring_exchange`, one xGMI link per rank pair) and the addition runs in the main
+rank's fused repair kernel; `pipelined_ring_repair` overlaps chunk c's transfer with the kernels of
+the chunks around it.
 """
 from __future__ import annotations
 
@@ -118,3 +125,71 @@ def gather_checksums(c: int, r: Rank, device="cpu") -> list[int]:
     out = [torch.zeros_like(t) for _ in range(r.world)]
     dist.all_gather(out, t)
     return [int(x.item()) & _MASK64 for x in out]
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class _Staged:
+    """gloo + CUDA tensors: gloo moves host tensors, so the chunk is staged through host memory."""
+
+    def __init__(self, works, host_recv, recv):
+        self.works, self.host_recv, self.recv = works, host_recv, recv
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.recv.copy_(self.host_recv)
+
+
+def ring_exchange(send: torch.Tensor, recv: torch.Tensor, r: Rank):
+    """Post send -> rank + 1 and recv <- rank - 1 (mod world) of two contiguous tensors of one shape;
+    returns a handle whose wait() makes the data usable (on nccl: the current stream waits for RCCL's).
+    With one rank the block stays where it is (recv = send)."""
+    if send.shape != recv.shape or not send.is_contiguous() or not recv.is_contiguous():
+        raise ValueError("ring_exchange: send and recv must be contiguous tensors of one shape")
+    if not r.distributed:
+        if recv.data_ptr() != send.data_ptr():
+            recv.copy_(send)
+        return _Done()
+    nxt, prv = (r.rank + 1) % r.world, (r.rank - 1) % r.world
+    if _BACKEND == "gloo" and send.is_cuda:
+        hs = send.cpu()
+        hr = torch.empty_like(hs)
+        works = dist.batch_isend_irecv([dist.P2POp(dist.isend, hs, nxt), dist.P2POp(dist.irecv, hr, prv)])
+        return _Staged(works, hr, recv)
+    works = dist.batch_isend_irecv([dist.P2POp(dist.isend, send, nxt), dist.P2POp(dist.irecv, recv, prv)])
+
+    class _Works:
+        def wait(self):
+            for w in works:
+                w.wait()
+    return _Works()
+
+
+def pipelined_ring_repair(n_stripes: int, chunk: int, helper, main, send, recv, r: Rank) -> None:
+    """Cross-GPU partial decoding over a ring of ranks, chunk by chunk.
+
+    Rank r is the helper proxy for the next rank's stripes and the main proxy for its own; stripe i's
+    helper partial is send[i] here and recv[i] on rank r + 1.  For every chunk [c0, c1):
+      helper(c0, c1)  -- launch the helper-partial kernel writing send[c0:c1]
+      ring_exchange   -- send[c0:c1] -> rank + 1, recv[c0:c1] <- rank - 1 (queued behind the kernel)
+      main(c0, c1)    -- after the chunk arrived: the main rank's fused kernel (own partial + addition)
+    The main kernel of chunk c is issued after the helper kernel and the transfer of chunk c + 1, so
+    transfers run back to back while the kernels fill the gaps."""
+    if chunk < 1:
+        raise ValueError("chunk must be >= 1")
+    spans = [(c, min(c + chunk, n_stripes)) for c in range(0, n_stripes, chunk)]
+    pending = None
+    for c0, c1 in spans:
+        helper(c0, c1)
+        h = ring_exchange(send[c0:c1], recv[c0:c1], r)
+        if pending is not None:
+            pending[0].wait()
+            main(*pending[1])
+        pending = (h, (c0, c1))
+    if pending is not None:
+        pending[0].wait()
+        main(*pending[1])

@@ -92,3 +92,95 @@ def test_stripe_range_single_and_uneven():
             sizes = [b - a for a, b in spans]
             assert max(sizes) - min(sizes) <= 1
     assert D.data_word_offset(3, 14, 1 << 20) == 3 * 14 * (1 << 20) // 8
+
+
+def _ring_worker(rank, world, port, S, chunk, q):
+    """Cross-GPU partial decoding (ecg_dist.pipelined_ring_repair) with gloo and host tensors: rank r is
+    the helper proxy for rank r + 1's stripes.  The partial arithmetic is the oracle's (CPU stand-in for
+    the kernels); what is under test is the ring routing, the chunk pipeline and the wait points."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import ecg_dist as D
+    from bench import azure_local_split
+    from oracle import ec_ref as E
+    from oracle import ref
+    r = D.from_env()
+    D.init(r, backend="gloo")
+    B, n = 64, 16
+    cp = E.CodingParameters(k=12, l=2, g=2, local_or_column=True)
+    ec = E.ec_factory(E.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)  # local_or_column reaches the object here (handle_repair.cpp:14)
+    cls_local = [e for e in range(n) if e not in (12, 13)]
+
+    def stripe(gs):  # global stripe gs: 16 blocks
+        data = [ref.splitmix_bytes(0xEC0DE, (gs * n + j) * B // 8, B) for j in range(12)]
+        coding = E.zeros(4, B)
+        ec.encode(data, coding, B)
+        return data + coding
+
+    def partial(blocks, e, which):
+        surv, sets = azure_local_split(e)
+        out = E.zeros(1, B)
+        ec.encode_partial_blocks_for_decoding([blocks[b] for b in sets[which]], out, B, sets[which], surv, [e])
+        return out[0]
+
+    nxt = (rank + 1) % world
+    send = torch.zeros((S, B), dtype=torch.uint8)
+    recv = torch.zeros((S, B), dtype=torch.uint8)
+    rebuilt = np.zeros((S, B), np.uint8)
+    calls = []
+
+    def helper(c0, c1):
+        calls.append(("h", c0, c1))
+        for i in range(c0, c1):
+            gs = nxt * S + i
+            send[i] = torch.from_numpy(partial(stripe(gs), cls_local[gs % 14], 0))
+
+    def main(c0, c1):
+        calls.append(("m", c0, c1))
+        for i in range(c0, c1):
+            gs = rank * S + i
+            rebuilt[i] = partial(stripe(gs), cls_local[gs % 14], 1) ^ recv[i].numpy()
+
+    D.pipelined_ring_repair(S, chunk, helper, main, send, recv, r)
+    ok = all(np.array_equal(rebuilt[i], stripe(rank * S + i)[cls_local[(rank * S + i) % 14]]) for i in range(S))
+    q.put((rank, ok, calls))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,S,chunk", [(2, 5, 2), (3, 4, 4)])
+def test_ring_partial_repair(world, S, chunk):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, S, chunk, q)) for r in range(world)]
+    [p.start() for p in procs]
+    res = sorted(q.get(timeout=120) for _ in procs)
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok, _ in res), res
+    # helper of chunk c + 1 is issued before the main kernel of chunk c
+    spans = [(c, min(c + chunk, S)) for c in range(0, S, chunk)]
+    want = [("h",) + spans[0]]
+    for i in range(1, len(spans)):
+        want += [("h",) + spans[i], ("m",) + spans[i - 1]]
+    want.append(("m",) + spans[-1])
+    assert res[0][2] == want
+
+
+def test_ring_exchange_single_rank_and_shape_checks():
+    sys.path[:0] = [os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    import ecg_dist as D
+    r = D.Rank(0, 1, 0)
+    a = torch.arange(12, dtype=torch.uint8).reshape(3, 4)
+    b = torch.zeros_like(a)
+    D.ring_exchange(a, b, r).wait()
+    assert torch.equal(a, b)
+    D.ring_exchange(a, a, r).wait()  # one rank, in place: nothing moves
+    with pytest.raises(ValueError):
+        D.ring_exchange(a, torch.zeros(4, 3, dtype=torch.uint8), r)
+    with pytest.raises(ValueError):
+        D.ring_exchange(a.t(), torch.zeros(4, 3, dtype=torch.uint8), r)
+    with pytest.raises(ValueError):
+        D.pipelined_ring_repair(3, 0, None, None, a, b, r)

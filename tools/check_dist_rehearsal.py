@@ -26,9 +26,9 @@ print(f"rs-encode-decode: N=1 512 stripes {c1:016x}; N=2 x 256 {c2:016x}; n_gpus
 ok &= c1 == c2 and rs2["n_gpus"] == 2 and len(rs2["parity_checksums"]) == 2
 print(f"rs4m-waves: N=1 {w1['parity_checksum']}; N=2 {w2['parity_checksum']}")
 ok &= w1["parity_checksum"] == w2["parity_checksum"]
-for f in ("lrc_n2", "pc_n2"):
+for f in ("lrc_n2", "pc_n2", "ring_n2"):
     x = line(f"{d}/{f}.log")
-    print(f, "n_gpus", x["n_gpus"])
-    ok &= x["n_gpus"] == 2
+    print(f, "n_gpus", x["n_gpus"], "verified", x.get("verified", "-"))
+    ok &= x["n_gpus"] == 2 and x.get("verified", True) is True
 print("REHEARSAL", "OK" if ok else "MISMATCH")
 sys.exit(0 if ok else 1)

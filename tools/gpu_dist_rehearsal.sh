@@ -14,6 +14,7 @@ run1 --workload rs4m-waves --stripes 2048 --block-size 1048576 > $O/waves_n1.log
 run2 --workload rs4m-waves --stripes 2048 --block-size 1048576 > $O/waves_n2.log 2>&1 && echo "waves n2 ok" &&
 run2 --workload lrc-repair --stripes 256 > $O/lrc_n2.log 2>&1 && echo "lrc n2 ok" &&
 run2 --workload pc-merge --stripes 64 > $O/pc_n2.log 2>&1 && echo "pc n2 ok" &&
+run2 --workload lrc-repair-ring --stripes 128 --chunk 32 > $O/ring_n2.log 2>&1 && echo "ring n2 ok" &&
 python tools/check_dist_rehearsal.py $O
 rc=$?
 [ $rc -eq 0 ] || { for f in $O/*.log; do echo "== $f"; grep -v amdgpu.ids $f | tail -8; done; }
