@@ -395,6 +395,7 @@ def ring_repair_state(r, S, B, chunk):
         surv, sets = azure_local_split(e)
         helper_progs.append((ec.partial_decoding_matrix(sets[0], surv, [e]), sets[0], [n]))
         main_progs.append(([list(ec.partial_decoding_matrix(sets[1], surv, [e])) + [1]], sets[1] + [n], [0]))
+    helper_progs, main_progs = ecg.Programs(helper_progs), ecg.Programs(main_progs)
 
     def make_store(owner):
         st = torch.empty((n + 1, S, B), dtype=torch.uint8, device="cuda")

@@ -390,24 +390,40 @@ def matrix_apply_batch(coef, src_ids, dst_ids, d_in, d_out, stream=None):
                                                B, S, _stream(stream)), "matrix_apply_batch")
 
 
+class Programs:
+    """Same-shape programs (coef [n_out][n_in], src_ids, dst_ids) packed once into the C arrays
+    matrix_apply_batch_multi passes; re-packing per call is most of a launch's Python-side cost, which
+    matters when a batch is issued in chunks (ecg_dist.pipelined_ring_repair)."""
+
+    def __init__(self, programs):
+        programs = list(programs)
+        if not programs:
+            raise EcgError(ECG_EINVAL, "matrix_apply_batch_multi: no programs")
+        self.n_prog = len(programs)
+        self.k_in, self.m_out = len(programs[0][1]), len(programs[0][2])
+        coefs, srcs, dsts = [], [], []
+        for coef, src, dst in programs:
+            if len(src) != self.k_in or len(dst) != self.m_out:
+                raise EcgError(ECG_EINVAL, "matrix_apply_batch_multi: programs differ in shape")
+            c = np.asarray(coef, dtype=np.int64).reshape(self.m_out, self.k_in)
+            coefs += list(c.ravel())
+            srcs += list(src)
+            dsts += list(dst)
+        self.coefs, self.srcs, self.dsts = _ints(coefs), _ints(srcs), _ints(dsts)
+
+
 def matrix_apply_batch_multi(programs, d_in, d_out, prog_of_stripe=None, stripe_of=None, n_launch=None,
                              stream=None):
-    """programs: list of (coef [n_out][n_in], src_ids, dst_ids), all of the same shape.  Launch stripe
-    i runs programs[prog_of_stripe[i]] on stripe stripe_of[i] (int32 CUDA tensors; None = identity)."""
-    n_prog = len(programs)
-    k_in, m_out = len(programs[0][1]), len(programs[0][2])
-    coefs, srcs, dsts = [], [], []
-    for coef, src, dst in programs:
-        c = np.asarray(coef, dtype=np.int64).reshape(m_out, k_in)
-        coefs += list(c.ravel())
-        srcs += list(src)
-        dsts += list(dst)
+    """programs: list of (coef [n_out][n_in], src_ids, dst_ids), all of the same shape, or a Programs.
+    Launch stripe i runs programs[prog_of_stripe[i]] on stripe stripe_of[i] (int32 CUDA tensors; None =
+    identity)."""
+    P = programs if isinstance(programs, Programs) else Programs(programs)
     _, _, B = d_in.shape
     S = n_launch if n_launch is not None else (stripe_of.numel() if stripe_of is not None else d_in.shape[0])
     iss, ibs = _strides(d_in)
     oss, obs = _strides(d_out)
     return _check(lib().ecg_matrix_apply_batch_multi(
-        n_prog, k_in, m_out, _ints(coefs), _ints(srcs), _ints(dsts),
+        P.n_prog, P.k_in, P.m_out, P.coefs, P.srcs, P.dsts,
         prog_of_stripe.data_ptr() if prog_of_stripe is not None else None,
         stripe_of.data_ptr() if stripe_of is not None else None,
         d_in.data_ptr(), iss, ibs, d_out.data_ptr(), oss, obs, B, S, _stream(stream)), "matrix_apply_batch_multi")

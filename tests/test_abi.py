@@ -243,3 +243,14 @@ def test_make_decode_matrix_equals_library_decode(ecg, oracle, k, m, row_k_ones)
     with pytest.raises(ecg.EcgError) as e:
         ecg.make_decode_matrix(k, m, M, row_k_ones, list(range(m + 1)))
     assert e.value.code == ecg.ECG_EUNDECODABLE
+
+
+def test_programs_packing_and_shape_checks(ecg):
+    """ecg.Programs packs same-shape programs once (what matrix_apply_batch_multi passes to the C ABI)."""
+    P = ecg.Programs([([[1, 2, 3]], [0, 1, 2], [5]), ([[4, 5, 6]], [3, 4, 6], [7])])
+    assert (P.n_prog, P.k_in, P.m_out) == (2, 3, 1)
+    assert list(P.coefs) == [1, 2, 3, 4, 5, 6] and list(P.srcs) == [0, 1, 2, 3, 4, 6] and list(P.dsts) == [5, 7]
+    with pytest.raises(ecg.EcgError):
+        ecg.Programs([])
+    with pytest.raises(ecg.EcgError):
+        ecg.Programs([([[1, 2]], [0, 1], [5]), ([[1, 2, 3]], [0, 1, 2], [5])])
