@@ -57,6 +57,7 @@ int ecg_set_device(int device) { return hipSetDevice(device) == hipSuccess ? ECG
 void ecg_free(void* p) { free(p); }
 
 int ecg_program_cache_size(void) { return (int)Engine::instance().cache_size(); }
+int ecg_host_contexts(void) { return Engine::instance().host_contexts(); }
 
 int ecg_batch_begin(void) { return batch_begin(); }
 int ecg_batch_flush(void) { return batch_flush(); }

@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <unordered_set>
 
 namespace ecg {
@@ -27,9 +28,13 @@ Engine* g_engines[kMaxDevices] = {};
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// Per-thread, per-device host-tier state: a non-blocking stream and a growable device scratch.
-struct ThreadCtx {
-    int device = -1;
+// Host-tier state: a non-blocking stream, a growable device scratch, a pinned staging area and the
+// host-batch pipeline's streams and slots.  Contexts are pooled per device and LEASED for the duration
+// of one synchronous host-tier call, so these resources are bounded by the number of calls in flight
+// at once -- not by the number of threads that ever called.  (The reference's proxy runs every SET on
+// a new detached thread, proxy.cpp:416-419; per-thread state would leak a stream, scratch and pinned
+// memory per request.)  Contexts live for the process.
+struct HostCtx {
     hipStream_t stream = nullptr;
     uint8_t* scratch = nullptr;
     size_t cap = 0;
@@ -43,14 +48,48 @@ struct ThreadCtx {
     uint8_t* pinned = nullptr;      // host view
     uint8_t* pinned_dev = nullptr;  // device view (mapped, fine-grained)
     size_t pinned_cap = 0;
-    ~ThreadCtx() {
-        // Process teardown may already have destroyed the runtime; leak rather than fault.
-    }
 };
 
-thread_local ThreadCtx t_ctx[kMaxDevices];
+std::mutex g_ctx_mu[kMaxDevices];
+// never destroyed (process lifetime, like the engines): no teardown-order hazard with late callers
+std::vector<HostCtx*>* const g_ctx_free = new std::vector<HostCtx*>[kMaxDevices];
+int g_ctx_created[kMaxDevices] = {};
 
-ThreadCtx& tctx(int device) { return t_ctx[device]; }
+class CtxLease {
+public:
+    explicit CtxLease(int device) : dev_(device) {
+        std::lock_guard<std::mutex> lk(g_ctx_mu[dev_]);
+        if (!g_ctx_free[dev_].empty()) {
+            c_ = g_ctx_free[dev_].back();
+            g_ctx_free[dev_].pop_back();
+        } else {
+            c_ = new HostCtx();
+            g_ctx_created[dev_]++;
+        }
+    }
+    ~CtxLease() {
+        if (!idle_) {
+            // a call that failed part-way may have left copies in flight: drain before the next lessee
+            if (c_->stream) (void)hipStreamSynchronize(c_->stream);
+            for (hipStream_t s : c_->pstream)
+                if (s) (void)hipStreamSynchronize(s);
+        }
+        std::lock_guard<std::mutex> lk(g_ctx_mu[dev_]);
+        g_ctx_free[dev_].push_back(c_);
+    }
+    CtxLease(const CtxLease&) = delete;
+    CtxLease& operator=(const CtxLease&) = delete;
+    HostCtx& operator*() { return *c_; }
+    int done() {  // the call completed and synchronised its streams
+        idle_ = true;
+        return ECG_OK;
+    }
+
+private:
+    int dev_;
+    HostCtx* c_;
+    bool idle_ = false;
+};
 
 }  // namespace
 
@@ -78,13 +117,9 @@ Engine& Engine::instance() {
     return *g_engines[dev];
 }
 
-hipStream_t Engine::thread_stream() {
-    ThreadCtx& c = tctx(device_);
-    if (!c.stream) {
-        if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) c.stream = nullptr;
-        c.device = device_;
-    }
-    return c.stream;
+int Engine::host_contexts() const {
+    std::lock_guard<std::mutex> lk(g_ctx_mu[device_]);
+    return g_ctx_created[device_];
 }
 
 size_t Engine::cache_size() {
@@ -259,18 +294,20 @@ bool same_ops(const std::vector<LinearOp>& a, const std::vector<LinearOp>& b) {
     return true;
 }
 
-// Pointer tables for pointer-table launches: per-thread ring of pinned host + device slots, a slot
-// reused only after the launch that read it has completed (its event).
+// Pointer tables for pointer-table launches: a per-device ring of pinned host + device slots shared by
+// all threads (process lifetime, so no per-thread leak), each slot locked while it is filled and its
+// launch enqueued, and reused only after that launch has completed (its event).
 struct TableSlot {
+    std::mutex mu;
     void* host = nullptr;
     void* dev = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
     bool pending = false;
 };
-constexpr int kTableSlots = 4;
-thread_local TableSlot t_tables[kMaxDevices][kTableSlots];
-thread_local int t_table_next[kMaxDevices] = {};
+constexpr int kTableSlots = 16;
+TableSlot g_tables[kMaxDevices][kTableSlots];
+std::atomic<unsigned> g_table_next[kMaxDevices];
 
 }  // namespace
 
@@ -346,8 +383,8 @@ int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* c
                           hipStream_t st) {
     const int S = (int)calls.size(), k = op.k_in(), m = op.m_out();
     const size_t n = (size_t)S * (k + m);
-    TableSlot& t = t_tables[device_][t_table_next[device_]];
-    t_table_next[device_] = (t_table_next[device_] + 1) % kTableSlots;
+    TableSlot& t = g_tables[device_][g_table_next[device_].fetch_add(1, std::memory_order_relaxed) % kTableSlots];
+    std::lock_guard<std::mutex> lk(t.mu);
     if (t.pending) {
         ECG_HIP(hipEventSynchronize(t.ev));
         t.pending = false;
@@ -417,7 +454,7 @@ int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks,
 // Host-buffer tier (the reference's per-stripe calls on host memory).  Device slots are assigned to the
 // blocks that must be uploaded first (read before any op writes them), then to the rest, so the
 // inputs form one contiguous range.  Small calls (the proxy's 1 KiB - 64 KiB blocks) gather those
-// inputs into a per-thread pinned staging area with memcpy and move them with ONE H2D copy, and bring
+// inputs into the leased context's pinned staging area with memcpy and move them with ONE H2D copy, and bring
 // every written block back with ONE D2H copy: two DMA transfers per call instead of one pageable copy
 // per block (each pageable copy is a driver-staged round trip).  Large calls copy block by block.
 int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B) {
@@ -427,8 +464,10 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         if (rc != ECG_OK) return rc;
     }
     if (ops.empty() || B == 0) return ECG_OK;
-    hipStream_t st = thread_stream();
-    if (!st) return ECG_EHIP;
+    CtxLease lease(device_);
+    HostCtx& c = *lease;
+    if (!c.stream) ECG_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    hipStream_t st = c.stream;
     std::vector<char> upload(nblocks, 0), written(nblocks, 0), used(nblocks, 0);
     {
         std::vector<char> produced(nblocks, 0);
@@ -452,7 +491,6 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
     for (int id = 0; id < nblocks; id++)
         if (used[id] && slot[id] < 0) slot[id] = nslots++;
     const size_t pitch = ((size_t)B + 255) & ~(size_t)255;
-    ThreadCtx& c = tctx(device_);
     if (c.cap < pitch * nslots) {
         ECG_HIP(hipStreamSynchronize(st));
         if (c.scratch) (void)hipFree(c.scratch);
@@ -493,7 +531,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         ECG_HIP(hipStreamSynchronize(st));
         for (int id = 0; id < nblocks; id++)
             if (written[id]) memcpy(blocks[id], c.pinned + (size_t)slot[id] * pitch, (size_t)B);
-        return ECG_OK;
+        return lease.done();
     }
     if (staged) {
         for (int id = 0; id < nblocks; id++)
@@ -543,7 +581,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         } else {
             ECG_HIP(hipStreamSynchronize(st));
         }
-        return ECG_OK;
+        return lease.done();
     }
     int id = 0;
     while (id < nblocks) {
@@ -557,7 +595,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         id = j;
     }
     ECG_HIP(hipStreamSynchronize(st));
-    return ECG_OK;
+    return lease.done();
 }
 
 int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of_stripe, int S,
@@ -642,7 +680,8 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     const int kin = prog.k_in(), mout = prog.m_out();
     const size_t pitch = ((size_t)B + 255) & ~(size_t)255;
     const size_t slot_in = (size_t)chunk * kin * pitch, slot_out = (size_t)chunk * mout * pitch;
-    ThreadCtx& c = tctx(device_);
+    CtxLease lease(device_);
+    HostCtx& c = *lease;
     if (!c.pipe_ready) {
         for (int i = 0; i < 3; i++) {
             ECG_HIP(hipStreamCreateWithFlags(&c.pstream[i], hipStreamNonBlocking));
@@ -713,7 +752,7 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
         used[slot] = true;
     }
     ECG_HIP(hipStreamSynchronize(s_out));
-    return ECG_OK;
+    return lease.done();
 }
 
 }  // namespace ecg

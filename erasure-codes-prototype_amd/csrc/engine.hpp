@@ -3,13 +3,14 @@
 // Four ways in (plus run_host_pipeline for host-resident batches):
 //   run_device  - block pointers are device pointers (HBM-resident), asynchronous on a stream;
 //   run_host    - block pointers are host buffers (the reference's char** of host memory): blocks are
-//                 staged into per-thread device scratch, each block copied in at most once and every
+//                 staged into the device scratch of a pooled host context leased for the call, each block copied in at most once and every
 //                 written block copied back once, then the stream is synchronised; small calls gather
 //                 through a pinned staging area so a call costs one H2D and one D2H transfer;
 //   run_strided - batches of S stripes laid out as base + stripe/block strides, each stripe running
 //                 one of a small set of programs (e.g. 14 rotating single-erasure decode patterns).
 // Coefficient tables are built on the host once per distinct program set and cached in HBM.
-// Thread-safe: the cache is mutex-protected; host-tier scratch and streams are per thread.
+// Thread-safe: the cache is mutex-protected; host-tier scratch and streams belong to pooled contexts,
+// one leased per call in flight.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -65,7 +66,7 @@ public:
                           int chunk_stripes);
 
     std::shared_ptr<ProgramSet> program_set(const std::vector<LinearOp>& progs, int* status);
-    hipStream_t thread_stream();  // per-thread non-blocking stream used by the host tier
+    int host_contexts() const;  // host-tier contexts created so far (pooled; bounded by concurrent calls)
     int device() const { return device_; }
     size_t cache_size();
 

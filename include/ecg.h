@@ -42,6 +42,11 @@ int ecg_device_count(void);
 int ecg_set_device(int device);    /* selects the HIP device for the calling thread */
 void ecg_free(void* p);            /* frees matrices returned by this library (malloc'd, like Jerasure) */
 int ecg_program_cache_size(void);  /* programs cached for the current device (diagnostics) */
+/* Host-tier contexts (stream + device scratch + pinned staging) created so far for the current device
+ * (diagnostics).  Contexts are pooled and leased per call, so this is bounded by the most host-tier calls
+ * ever in flight at once, not by the number of threads that called (the reference's proxy starts a
+ * thread per request, proxy.cpp:416-419). */
+int ecg_host_contexts(void);
 
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
  * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP).  Results never depend on them. */

@@ -94,3 +94,42 @@ def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle):
     finally:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
     assert not errors, errors[:5]
+
+
+def test_thread_per_request_resources_bounded(ecg, oracle):
+    """The proxy starts a new detached thread per SET (proxy.cpp:416-419) and calls the codec from it.
+    Host-tier contexts (stream, device scratch, pinned staging) are leased per call from a pool, so 240
+    short-lived threads, at most 6 alive at once, create at most 6 new contexts; pointer-table slots are
+    per device, not per thread.  Every result is checked against the oracle."""
+    import torch
+    from oracle import ec_ref as E
+    before = ecg.lib().ecg_host_contexts()
+    errors = []
+    o = E.ec_factory(0, E.CodingParameters(k=6, m=3))
+
+    def one(i):
+        try:
+            p = ecg.ec_factory(0, ecg.CodingParameters(k=6, m=3))
+            B = 4096 if i % 3 else 300 * 1024
+            data = [np.random.default_rng(i * 10 + j).integers(0, 256, B, dtype=np.uint8) for j in range(6)]
+            ref = E.zeros(3, B)
+            o.encode(data, ref, B)
+            got = [np.zeros(B, np.uint8) for _ in range(3)]
+            assert p.encode(data, got, B) == 0
+            assert all(np.array_equal(a, b) for a, b in zip(got, ref)), ("host", i)
+            if i % 4 == 0:  # pointer-table launch (region_xor_batch) from this short-lived thread
+                a = torch.from_numpy(np.stack(data[:2])).cuda()
+                b = torch.from_numpy(np.stack(data[2:4])).cuda()
+                ecg.region_xor_batch(a, b)
+                torch.cuda.current_stream().synchronize()
+                assert np.array_equal(b.cpu().numpy(), np.stack(data[:2]) ^ np.stack(data[2:4])), ("xor", i)
+        except Exception as e:  # noqa: BLE001
+            errors.append((i, repr(e)))
+
+    for wave in range(40):
+        th = [threading.Thread(target=one, args=(wave * 6 + t,)) for t in range(6)]
+        [x.start() for x in th]
+        [x.join(timeout=60) for x in th]
+        assert not any(x.is_alive() for x in th), "a worker hung"
+    assert not errors, errors[:5]
+    assert ecg.lib().ecg_host_contexts() - before <= 6

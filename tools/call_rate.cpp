@@ -2,7 +2,8 @@
 // stripe (proxy.cpp:312-349); with HBM-resident blocks each such call is one asynchronous launch.  This
 // measures how many per-stripe calls per second the C ABI sustains (host issue cost) and the resulting
 // data rate, against one batched launch over the same stripes.
-// Build: hipcc -O2 -std=c++17 -I../include tools/call_rate.cpp -L.../lib -lecg
+// Build: hipcc -O2 -std=c++20 --offload-arch=gfx950 -Iinclude tools/call_rate.cpp -Lerasure-codes-prototype_amd/lib -lecg
+//        -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o tools/call_rate
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -147,6 +148,30 @@ int main(int argc, char** argv) {
                    T * calls / dt, dt / calls * 1e6, errors ? "  ERRORS" : "");
             fflush(stdout);
         }
+        ecg_free(Mh);
+    }
+    // Thread per request (the proxy starts a detached thread per SET and encodes on it, proxy.cpp:416-419):
+    // each request is a new thread making ONE host-tier call.  Reported with the bare thread start/join
+    // cost alongside, so the difference is what the library adds to a cold thread's first call.
+    for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 65536}, {10, 4, 1 << 20}}) {
+        int* Mh = ecg_reed_sol_vandermonde_coding_matrix(kk, mm, 8);
+        std::vector<std::vector<char>> blocks(kk + mm, std::vector<char>(B, 3));
+        std::vector<char*> p(kk + mm);
+        for (int i = 0; i < kk + mm; i++) p[i] = blocks[i].data();
+        const int reqs = B >= (1 << 20) ? 100 : 500;
+        std::atomic<int> errors{0};
+        double t0 = now();
+        for (int r = 0; r < reqs; r++) std::thread([] {}).join();
+        const double bare = (now() - t0) / reqs * 1e6;
+        t0 = now();
+        for (int r = 0; r < reqs; r++)
+            std::thread([&] {
+                if (ecg_jerasure_matrix_encode(kk, mm, 8, Mh, p.data(), p.data() + kk, B) != 0) errors++;
+            }).join();
+        const double per = (now() - t0) / reqs * 1e6;
+        printf("thread per request RS(%d,%d) B=%7d: %7.1f us/request (bare thread %.1f us)%s\n", kk, mm, B, per, bare,
+               errors ? "  ERRORS" : "");
+        fflush(stdout);
         ecg_free(Mh);
     }
     ecg_free(M);
