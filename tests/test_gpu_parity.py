@@ -1017,3 +1017,65 @@ def test_region_xor_batch(ecg, oracle, torch_cuda):
         c = b.copy()
         oracle.galois_region_xor(a, c, n)  # self-inverse: XOR the source back in
         assert np.array_equal(c, b ^ a)
+
+
+@pytest.mark.parametrize("isvertical", [True, False])
+@pytest.mark.parametrize("seri_num", [0, 1])
+def test_hpc_orientation_vs_oracle(ecg, oracle, torch_cuda, isvertical, seri_num):
+    """HPC::isvertical (pc.h:65) picks which dimension uses the enlarged RS code (pc.cpp:585-619,
+    680-728, 755-835): the merged-stripe orientation of config 4.  Encode, decode and the partial
+    encodings / decodings of one row and one column, for both orientations, against the oracle."""
+    from oracle import ec_ref as E
+    params = dict(k1=4, m1=2, k2=2, m2=1, x=2, seri_num=seri_num)
+    cp = E.CodingParameters(**params)
+    o = E.ec_factory(8, cp)
+    o.init_coding_parameters(cp)
+    o.isvertical = isvertical
+    p = ecg.ec_factory(8, ecg.CodingParameters(**params))
+    p.init_coding_parameters(ecg.CodingParameters(**params))
+    p.set_isvertical(isvertical)
+    B = 2048 + 7
+    rng = random.Random(seri_num * 2 + isvertical)
+    data = E.blocks(o.k, B, 11 + seri_num)
+    ca, cb = E.zeros(o.m, B), E.zeros(o.m, B)
+    o.encode(data, ca, B)
+    assert p.encode(data, cb, B) == 0
+    assert same(ca, cb), "encode"
+    stripe = data + ca
+    n = o.k + o.m
+    for _ in range(8):
+        pat = rng.sample(range(n), rng.randint(1, 3))
+        A, Bq = [x.copy() for x in stripe], [x.copy() for x in stripe]
+        for i in pat:
+            A[i][:] = 0
+            Bq[i][:] = 0
+        ra = o.decode(A[:o.k], A[o.k:], B, pat + [-1], len(pat))
+        rb = p.decode(Bq[:o.k], Bq[o.k:], B, pat + [-1], len(pat))
+        assert (ra == 0) == (rb == 0), pat
+        assert same(A, Bq), ("decode", pat)
+    for local in (False, True):  # a row (global) or a column (local) of the grid
+        o.local_or_column = local
+        cpl = ecg.CodingParameters(**params, local_or_column=local)
+        p.init_coding_parameters(cpl)
+        p.set_isvertical(isvertical)
+        if local:
+            c = rng.randrange(o.k1)
+            members = [o.rowcol2bid(r, c) for r in range(o.k2 + o.m2)]
+            nd = o.k2
+        else:
+            r = rng.randrange(o.k2)
+            members = [o.rowcol2bid(r, c) for c in range(o.k1 + o.m1)]
+            nd = o.k1
+        d_all, par = members[:nd], members[nd:]
+        sub = rng.sample(d_all, rng.randint(1, nd))
+        a, b = E.zeros(len(par), B), E.zeros(len(par), B)
+        o.encode_partial_blocks_for_encoding([stripe[i] for i in sub], a, B, sub, par)
+        assert p.encode_partial_blocks_for_encoding([stripe[i] for i in sub], b, B, sub, par) == 0
+        assert same(a, b), ("partial enc", local, sub, par)
+        lost = rng.choice(members)
+        surv = [i for i in members if i != lost][:nd]
+        lsub = rng.sample(surv, rng.randint(1, nd))
+        a, b = E.zeros(1, B), E.zeros(1, B)
+        o.encode_partial_blocks_for_decoding([stripe[i] for i in lsub], a, B, lsub, surv, [lost])
+        assert p.encode_partial_blocks_for_decoding([stripe[i] for i in lsub], b, B, lsub, surv, [lost]) == 0
+        assert same(a, b), ("partial dec", local, lsub, surv, lost)
