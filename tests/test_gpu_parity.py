@@ -836,11 +836,18 @@ def test_batch_scope_per_stripe_calls(ecg, oracle, torch_cuda):
     ecg.encode_batch(k, m, M, ref[:, :k], ref[:, k:])
     st[:, k:] = 0x5A
     ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
-    with ecg.batch():
-        for s in range(S):
+    with ecg.batch() as scope:
+        for s in range(S // 2):
             ec.encode([st[s, j] for j in range(k)], [st[s, k + i] for i in range(m)], B)
         torch.cuda.synchronize()
         assert bool((st[:, k:] == 0x5A).all()), "deferred calls ran before the scope ended"
+        scope.flush()  # ecg_batch_flush: the recorded half is launched, the scope stays open
+        torch.cuda.synchronize()
+        assert torch.equal(st[:S // 2], ref[:S // 2])
+        for s in range(S // 2, S):
+            ec.encode([st[s, j] for j in range(k)], [st[s, k + i] for i in range(m)], B)
+        torch.cuda.synchronize()
+        assert bool((st[S // 2:, k:] == 0x5A).all()), "deferred calls ran before the scope ended"
     torch.cuda.synchronize()
     assert torch.equal(st, ref)
     # decode: runs of 8 stripes share an erasure pattern (one batched launch per run)

@@ -146,3 +146,30 @@ def test_planning_bad_arguments(ecg):
         rs.generate_repair_plan([6])
     with pytest.raises(ecg.EcgError):
         rs.grouping_information()
+
+
+def test_get_coding_parameters_per_family(ecg):
+    """get_coding_parameters writes the fields each class owns (erasure_code.cpp:12-17, lrc.cpp:14-21,
+    pc.cpp:20-29) and init_coding_parameters copies local_or_column where the reference does
+    (erasure_code.cpp:5-10, lrc.cpp:5-12) and not where it does not (ERS, rs.cpp:282-288)."""
+    E = ecg.ECTYPE
+    cp = ecg.CodingParameters
+    rs = ecg.ec_factory(E.RS, cp(k=10, m=4))
+    g = rs.get_coding_parameters()
+    assert (g.k, g.m, g.local_or_column) == (10, 4, False)
+    rs.init_coding_parameters(cp(k=6, m=3, local_or_column=True))
+    g = rs.get_coding_parameters()
+    assert (g.k, g.m, g.local_or_column, rs.k, rs.m) == (6, 3, True, 6, 3)
+    ers = ecg.ec_factory(E.ERS, cp(k=4, m=2, x=2, seri_num=1))
+    ers.init_coding_parameters(cp(k=4, m=2, x=2, seri_num=1, local_or_column=True))
+    assert ers.get_coding_parameters().local_or_column is False
+    az = ecg.ec_factory(E.AZURE_LRC, cp(k=12, l=2, g=2))
+    g = az.get_coding_parameters()
+    assert (g.k, g.l, g.g, g.m) == (12, 2, 2, 4)
+    az.init_coding_parameters(cp(k=12, l=2, g=2, local_or_column=True))
+    assert az.get_coding_parameters().local_or_column is True
+    pc = ecg.ec_factory(E.PC, cp(k1=4, m1=1, k2=4, m2=1))
+    g = pc.get_coding_parameters()
+    assert (g.k1, g.m1, g.k2, g.m2, g.k, g.m) == (4, 1, 4, 1, 16, 9)
+    hv = ecg.ec_factory(E.HV_PC, cp(k1=4, m1=1, k2=4, m2=1))
+    assert (hv.k, hv.m) == (16, 8)

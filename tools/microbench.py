@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true", help="defaults only: encode, decode, copy, 10->1 xor")
+    ap.add_argument("--only", default=None, help="run only the variants whose name contains this string")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     k, m, B, S = 10, 4, a.block, a.stripes
@@ -114,6 +115,8 @@ def main():
                              lambda: ecg.perform_addition_batch(1, 1, src1, dst1), 2 * halfS * B))
             variants.append((f"xor 10->1 map={gmap}", opt(3, 0, 0, gmap),
                              lambda: ecg.perform_addition_batch(10, 1, data, rebuilt), S * 11 * B))
+    if a.only:
+        variants = [v for v in variants if a.only in v[0]]
     res = {name: [] for name, *_ in variants}
     for r in range(a.rounds):
         for name, setup, fn, nbytes in variants:
