@@ -974,18 +974,22 @@ def test_program_cache_bounded(ecg, oracle, torch_cuda):
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
 
 
-def test_large_host_blocks_pinned_for_the_call(ecg, oracle, torch_cuda):
+def test_large_host_blocks(ecg, oracle, torch_cuda):
     """The reference's SET buffers (proxy.cpp:335-339): k slices of ONE contiguous value buffer and m
-    separate parity buffers, 1 MiB blocks.  The host tier pins them for the call (refcounted, so four
-    threads encoding from the same value buffer never unpin each other's pages) and returns the bytes
-    the oracle computes; the buffers stay ordinary pageable memory afterwards."""
-    k, m, B = 10, 4, 1 << 20
+    separate parity buffers, 1 MiB blocks, from four threads that share the value buffer as input.  The
+    large-block host path (pageable copies, contiguous runs coalesced, the caller's pages never
+    registered) returns the oracle's bytes for separate parity buffers, for parities forming one
+    odd-offset run inside a shared buffer (its neighbours untouched), and for an in-place decode whose
+    outputs are slices next to input slices."""
+    k, m, B = 10, 4, (1 << 20) + 5
     M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
     value = rnd(k * B, 4242)
     data = [value[j * B:(j + 1) * B] for j in range(k)]
     expect = [np.zeros(B, np.uint8) for _ in range(m)]
     oracle.jerasure_matrix_encode(k, m, M, data, expect, B)
-    outs = [[np.zeros(B, np.uint8) for _ in range(m)] for _ in range(4)]
+    shared = np.full(3 + m * B + 7, 0x77, np.uint8)  # thread 3: parities as one contiguous odd run
+    outs = [[np.zeros(B, np.uint8) for _ in range(m)] for _ in range(3)]
+    outs.append([shared[3 + i * B:3 + (i + 1) * B] for i in range(m)])
     errs = []
 
     def work(t):
@@ -1001,13 +1005,16 @@ def test_large_host_blocks_pinned_for_the_call(ecg, oracle, torch_cuda):
     assert not errs, errs
     for t in range(4):
         assert same(outs[t], expect), t
+    assert (shared[:3] == 0x77).all() and (shared[3 + m * B:] == 0x77).all()  # neighbours untouched
     # decode in place: lose data 3 and parity 1 (garbage in both), survivors are slices of `value`
     stripe = data + [x.copy() for x in expect]
+    orig = value.copy()
     lost = [stripe[3].copy(), stripe[k + 1].copy()]
     stripe[3][:] = 0xEE
     stripe[k + 1][:] = 0xEE
     assert ecg.jerasure_matrix_decode(k, m, M, 2, [3, k + 1, -1], stripe[:k], stripe[k:], B) == 0
     assert np.array_equal(stripe[3], lost[0]) and np.array_equal(stripe[k + 1], lost[1])
+    assert np.array_equal(value, orig)  # the rebuilt slice is exact and its neighbour slices untouched
 
 
 def test_region_xor_batch(ecg, oracle, torch_cuda):
