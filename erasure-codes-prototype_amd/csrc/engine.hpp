@@ -3,9 +3,10 @@
 // Four ways in (plus run_host_pipeline for host-resident batches):
 //   run_device  - block pointers are device pointers (HBM-resident), asynchronous on a stream;
 //   run_host    - block pointers are host buffers (the reference's char** of host memory): blocks are
-//                 staged into the device scratch of a pooled host context leased for the call, each block copied in at most once and every
-//                 written block copied back once, then the stream is synchronised; small calls gather
-//                 through a pinned staging area so a call costs one H2D and one D2H transfer;
+//                 staged into the device scratch of a pooled host context leased for the call, each
+//                 block copied in at most once and every written block copied back once, then the
+//                 stream is synchronised; small calls gather through a pinned staging area so a call
+//                 costs one H2D and one D2H transfer;
 //   run_strided - batches of S stripes laid out as base + stripe/block strides, each stripe running
 //                 one of a small set of programs (e.g. 14 rotating single-erasure decode patterns).
 // Coefficient tables are built on the host once per distinct program set and cached in HBM.
