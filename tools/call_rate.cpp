@@ -12,6 +12,7 @@
 #include <tuple>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "ecg.h"
@@ -101,6 +102,10 @@ int main(int argc, char** argv) {
         }
         ecg_ec_destroy(ec);
         CK(hipFree(buf));
+    }
+    if (argc > 2 && std::string(argv[2]) == "device") {  // device tier only (e.g. under rocprofv3)
+        ecg_free(M);
+        return 0;
     }
     // Host tier (synchronous calls on host buffers, the proxy's own buffers): latency per call from C++.
     for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 1024}, {10, 4, 16384}, {10, 4, 65536},
