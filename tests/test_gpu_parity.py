@@ -621,11 +621,13 @@ def test_matrix_apply_multi_with_stripe_subset(ecg, oracle, torch_cuda):
         assert np.array_equal(hout[s, 1], ref[0]) and np.array_equal(hout[s, 0], ref[1]), s
 
 
+@pytest.mark.parametrize("B,S", [(65536 + 48, 11), ((1 << 20) + 16, 9)])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_host_pipeline_encode_decode(ecg, oracle, torch_cuda, pinned):
-    """Host-resident batches through the H2D -> kernel -> D2H pipeline (chunks not dividing S)."""
+def test_host_pipeline_encode_decode(ecg, oracle, torch_cuda, pinned, B, S):
+    """Host-resident batches, pinned and pageable, through the H2D -> kernel -> D2H pipeline (chunks not
+    dividing S; 64 KiB and 1 MiB blocks)."""
     torch = torch_cuda
-    k, m, B, S = 10, 4, 65536 + 48, 11
+    k, m = 10, 4
     n = k + m
     M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
     if pinned:
