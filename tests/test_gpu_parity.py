@@ -1095,3 +1095,28 @@ def test_hpc_orientation_vs_oracle(ecg, oracle, torch_cuda, isvertical, seri_num
         o.encode_partial_blocks_for_decoding([stripe[i] for i in lsub], a, B, lsub, surv, [lost])
         assert p.encode_partial_blocks_for_decoding([stripe[i] for i in lsub], b, B, lsub, surv, [lost]) == 0
         assert same(a, b), ("partial dec", local, lsub, surv, lost)
+
+
+def test_block_larger_than_2gib(ecg, oracle, torch_cuda):
+    """One block of 2^31 + 53 bytes: the jerasure tier's `int size` cannot express it, the batched tier
+    takes 64-bit sizes.  Exercises 64-bit offsets in the vector kernel (2^31 + 48 bytes) and the byte
+    kernel's tail (5 bytes past it), GENERAL and BINARY, checked against the oracle on windows at the
+    start, across the 2 GiB boundary and at the end; the byte after the block stays untouched."""
+    torch = torch_cuda
+    Bmax = (1 << 31) + 64
+    B = (1 << 31) + 53
+    st = torch.empty((1, 4, Bmax), dtype=torch.uint8, device="cuda")  # 8 GiB
+    ecg.fill_random(st, 77)
+    st[0, 2:, B:] = 0xA5
+    view = st[:, :, :B]  # strides stay 16-byte multiples; B itself is ragged
+    ecg.matrix_apply_batch([[7, 201]], [0, 1], [2], view, view)   # GENERAL
+    ecg.matrix_apply_batch([[1, 1]], [0, 1], [3], view, view)     # BINARY
+    torch.cuda.synchronize()
+    for lo in (0, (1 << 31) - 4096, B - 6000):
+        hi = min(B, lo + 8192)
+        a, b = st[0, 0, lo:hi].cpu().numpy(), st[0, 1, lo:hi].cpu().numpy()
+        ref = [np.zeros(hi - lo, np.uint8)]
+        oracle.jerasure_matrix_encode(2, 1, [7, 201], [a, b], ref, hi - lo)
+        assert np.array_equal(st[0, 2, lo:hi].cpu().numpy(), ref[0]), lo
+        assert np.array_equal(st[0, 3, lo:hi].cpu().numpy(), a ^ b), lo
+    assert bool((st[0, 2:, B:] == 0xA5).all())
