@@ -1120,3 +1120,28 @@ def test_block_larger_than_2gib(ecg, oracle, torch_cuda):
         assert np.array_equal(st[0, 2, lo:hi].cpu().numpy(), ref[0]), lo
         assert np.array_equal(st[0, 3, lo:hi].cpu().numpy(), a ^ b), lo
     assert bool((st[0, 2:, B:] == 0xA5).all())
+
+
+def test_host_block_at_int_max(ecg, oracle, torch_cuda):
+    """The reference's largest expressible block (`int block_size` = 2^31 - 1) through the Jerasure tier
+    on host buffers: RS(2,1) encode and a decode of the lost data block, checked against the oracle on
+    windows at the start, across 1 GiB, and at the ragged end."""
+    torch = torch_cuda
+    B = (1 << 31) - 1
+    g = torch.empty((2, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(g, 91)
+    data = [g[0].cpu().numpy(), g[1].cpu().numpy()]
+    del g
+    M = ecg.reed_sol_vandermonde_coding_matrix(2, 1)
+    coding = [np.zeros(B, np.uint8)]
+    ecg.jerasure_matrix_encode(2, 1, M, data, coding, B)
+    wins = [(0, 8192), ((1 << 30) - 4096, (1 << 30) + 4096), (B - 8191, B)]
+    for lo, hi in wins:
+        ref = [np.zeros(hi - lo, np.uint8)]
+        oracle.jerasure_matrix_encode(2, 1, M, [data[0][lo:hi], data[1][lo:hi]], ref, hi - lo)
+        assert np.array_equal(coding[0][lo:hi], ref[0]), lo
+    saved = [data[0][lo:hi].copy() for lo, hi in wins]
+    data[0][:] = 0xEE
+    assert ecg.jerasure_matrix_decode(2, 1, M, 1, [0, -1], data, coding, B) == 0
+    for (lo, hi), want in zip(wins, saved):
+        assert np.array_equal(data[0][lo:hi], want), lo
