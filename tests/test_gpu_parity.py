@@ -1145,3 +1145,30 @@ def test_host_block_at_int_max(ecg, oracle, torch_cuda):
     assert ecg.jerasure_matrix_decode(2, 1, M, 1, [0, -1], data, coding, B) == 0
     for (lo, hi), want in zip(wins, saved):
         assert np.array_equal(data[0][lo:hi], want), lo
+
+
+def test_decode_duplicate_erasures(ecg, oracle, torch_cuda):
+    """Repeated ids in `erasures` count once (jerasure_erasures_to_erased), so [3, 3] decodes like [3]
+    and four distinct losses among repeats are still > m = 3 (-1): host tier and device tier agree with
+    the oracle, return codes included."""
+    torch = torch_cuda
+    k, m, B = 6, 3, 4096 + 9
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    data = [rnd(B, 300 + j) for j in range(k)]
+    coding = [np.zeros(B, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, data, coding, B)
+    for er in ([3, 3], [3, 7, 3, 7], [0, 8, 0, 8, 8], [1, 2, 3, 1, 2, 3, 4]):
+        A = [x.copy() for x in data + coding]
+        Bh = [x.copy() for x in data + coding]
+        for e in er:
+            A[e][:] = 0xEE
+            Bh[e][:] = 0xEE
+        ra = oracle.jerasure_matrix_decode(k, m, M, 1, er + [-1], A[:k], A[k:], B)
+        rb = ecg.jerasure_matrix_decode(k, m, M, 1, er + [-1], Bh[:k], Bh[k:], B)
+        assert ra == rb and same(A, Bh), er
+        dev = [torch.from_numpy(x).cuda() for x in [y.copy() for y in data + coding]]
+        for e in er:
+            dev[e].fill_(0xEE)
+        assert ecg.dev_matrix_decode(k, m, M, 1, er + [-1], dev[:k], dev[k:], B) == ra, er
+        torch.cuda.synchronize()
+        assert same([x.cpu().numpy() for x in dev], A), er  # undecodable: nothing written, as in the library
