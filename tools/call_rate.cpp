@@ -39,7 +39,17 @@ static double now() {
 }
 
 int main(int argc, char** argv) {
+    // CALL_RATE_SCHED=spin|yield|block: the application's hipSetDeviceFlags scheduling policy, which
+    // decides how hipStreamSynchronize waits (the host tier's per-call completion wait)
+    if (const char* sch = getenv("CALL_RATE_SCHED")) {
+        const std::string v(sch);
+        const unsigned f = v == "spin" ? hipDeviceScheduleSpin : v == "yield" ? hipDeviceScheduleYield
+                                                                               : hipDeviceScheduleBlockingSync;
+        CK(hipSetDeviceFlags(f));
+        printf("scheduling policy: %s\n", sch);
+    }
     const int k = 10, m = 4, n = k + m;
+    const bool host_latency_only = argc > 2 && std::string(argv[2]) == "latency";
     const int reps = argc > 1 ? atoi(argv[1]) : 3;
     int* M = ecg_reed_sol_vandermonde_coding_matrix(k, m, 8);
     hipStream_t st;
@@ -48,6 +58,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (long long B : {64LL << 10, 256LL << 10, 1LL << 20}) {
+        if (host_latency_only) break;
         const int S = (int)std::min(4096LL, (16LL << 30) / (n * B));
         uint8_t* buf;
         CK(hipMalloc(&buf, (size_t)S * n * B));
@@ -107,6 +118,7 @@ int main(int argc, char** argv) {
         ecg_free(M);
         return 0;
     }
+
     // Host tier (synchronous calls on host buffers, the proxy's own buffers): latency per call from C++.
     for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 1024}, {10, 4, 16384}, {10, 4, 65536},
                              {10, 4, 1 << 20}, {10, 4, 4 << 20}}) {
@@ -129,6 +141,10 @@ int main(int argc, char** argv) {
         printf("host tier RS(%d,%d) B=%6d  encode %6.1f us/call  decode %6.1f us/call\n", kk, mm, B, enc, dec);
         fflush(stdout);
         ecg_free(Mh);
+    }
+    if (host_latency_only) {
+        ecg_free(M);
+        return 0;
     }
     // Concurrent host-tier callers (the proxy runs encode on detached threads, proxy.cpp:416-419):
     // T threads, each with its own buffers, issuing synchronous RS(6,4) / RS(10,4) calls.
