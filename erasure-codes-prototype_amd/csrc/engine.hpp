@@ -58,6 +58,10 @@ public:
     // One op over S calls' block pointers (host arrays): uploads the pointer tables, then run_ptrs.
     int run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* const*>& call_blocks, long long B,
                       hipStream_t stream);
+    // The same, as ONE strided launch when the calls' blocks form base + call * sstride + id * bstride
+    // (checked pointer by pointer); *done = false (nothing launched) otherwise.
+    int run_calls_strided(const LinearOp& op, const std::vector<const uint8_t* const*>& calls, long long B,
+                          hipStream_t stream, bool* done);
 
     // Host-resident batch (block b of stripe s at h_in + s*in_sstride + b*in_bstride, likewise out):
     // a 3-slot pipeline of H2D (2-D copies of the blocks the program reads), kernel, D2H (the blocks
@@ -90,9 +94,10 @@ private:
 // Deferred-batch scope of the calling thread (ecg_batch_begin / ecg_batch_end).  Inside a scope,
 // device-tier calls (run_device: ecg_dev_matrix_*, ErasureCode objects on HBM buffers) are recorded
 // instead of launched; batch_flush() launches each run of consecutive calls with the same plan and
-// block size on the same stream as ONE pointer-table launch per op, splitting a run where a call
-// touches a block an earlier call of the run writes (or writes one it reads).  Host-tier and batched
-// calls flush first, so call order is kept.
+// block size on the same stream as ONE launch per op -- strided when the run's blocks form one strided
+// batch, a pointer-table launch otherwise -- splitting a run where a call touches a block an earlier
+// call of the run writes (or writes one it reads).  Host-tier and batched calls flush first, so call
+// order is kept.
 int batch_begin();
 int batch_flush();
 int batch_end();

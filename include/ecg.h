@@ -115,8 +115,10 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
  * launch cost (~8 us per RS(10,4) call).  Between ecg_batch_begin() and ecg_batch_end(), device-tier
  * calls of this thread (ecg_dev_matrix_* and ErasureCode handles in ECG_MEM_DEVICE mode) are only
  * validated and recorded; ecg_batch_end() (or ecg_batch_flush()) launches every run of consecutive
- * calls with the same plan, block size and stream as one pointer-table launch per op, asynchronously
- * on that stream.  Outputs are defined once the flush's work completes on the stream.  A run is split
+ * calls with the same plan, block size and stream as one launch per op, asynchronously on that
+ * stream: a strided launch when the run's blocks are one strided batch (block b of the c-th call at
+ * base + c * stripe_stride + b * block_stride, checked for every pointer), a pointer-table launch
+ * otherwise.  Outputs are defined once the flush's work completes on the stream.  A run is split
  * where a call reads or writes a block an earlier call of the run writes, or writes one it reads
  * (blocks compared by address: partially overlapping blocks are not allowed).  Host-tier and batched
  * calls made inside the scope flush first.  Scopes do not nest (ECG_EINVAL). */

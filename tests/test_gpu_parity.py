@@ -1172,3 +1172,48 @@ def test_decode_duplicate_erasures(ecg, oracle, torch_cuda):
         assert ecg.dev_matrix_decode(k, m, M, 1, er + [-1], dev[:k], dev[k:], B) == ra, er
         torch.cuda.synchronize()
         assert same([x.cpu().numpy() for x in dev], A), er  # undecodable: nothing written, as in the library
+
+
+@pytest.mark.parametrize("layout", ["strided", "scattered"])
+def test_batch_scope_layouts(ecg, oracle, torch_cuda, layout):
+    """A batch-scope run whose blocks form one strided batch goes out as a strided launch; scattered
+    blocks (random offsets in a pool) as a pointer-table launch.  Both give the oracle's bytes, for
+    encode and for a decode plan of several ops."""
+    torch = torch_cuda
+    k, m, S, B = 6, 3, 24, 8192 + 16
+    n = k + m
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    pool = torch.empty(((S * n + 7) * B,), dtype=torch.uint8, device="cuda")
+    if layout == "strided":
+        offs = [[(s * n + b) * B for b in range(n)] for s in range(S)]
+    else:
+        slots = list(range(S * n + 7))
+        random.Random(4).shuffle(slots)
+        offs = [[slots[s * n + b] * B for b in range(n)] for s in range(S)]
+    host = [[rnd(B, 1000 + s * n + b) for b in range(k)] for s in range(S)]
+    blk = [[pool[o:o + B] for o in offs[s]] for s in range(S)]
+    for s in range(S):
+        for b in range(k):
+            blk[s][b].copy_(torch.from_numpy(host[s][b]))
+        for b in range(k, n):
+            blk[s][b].fill_(0x5A)
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
+    with ecg.batch():
+        for s in range(S):
+            ec.encode(blk[s][:k], blk[s][k:], B)
+    torch.cuda.synchronize()
+    want = []
+    for s in range(S):
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode(k, m, M, host[s], ref, B)
+        want.append(host[s] + ref)
+        assert same([x.cpu().numpy() for x in blk[s]], want[s]), (layout, "encode", s)
+    for s in range(S):  # lose data 1 and parity 0 everywhere: one decode plan of several ops per call
+        blk[s][1].fill_(0xEE)
+        blk[s][k].fill_(0xEE)
+    with ecg.batch():
+        for s in range(S):
+            ec.decode(blk[s][:k], blk[s][k:], B, [1, k, -1], 2)
+    torch.cuda.synchronize()
+    for s in range(S):
+        assert same([x.cpu().numpy() for x in blk[s]], want[s]), (layout, "decode", s)
