@@ -317,7 +317,10 @@ int ecg_region_xor_batch(const void* d_src, long long src_stride, void* d_dst, l
         blk[s] = {(const uint8_t*)d_src + (size_t)s * src_stride, (const uint8_t*)d_dst + (size_t)s * dst_stride};
         calls[s] = blk[s].data();
     }
-    return Engine::instance().run_ptr_batch(op, calls, nbytes, (hipStream_t)stream);
+    Engine& e = Engine::instance();
+    bool done = false;  // regular strides (the usual case): the strided launch, else a pointer table
+    const int rc = e.run_calls_strided(op, calls, nbytes, (hipStream_t)stream, &done);
+    return done || rc != ECG_OK ? rc : e.run_ptr_batch(op, calls, nbytes, (hipStream_t)stream);
 }
 
 int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, long long in_sstride,

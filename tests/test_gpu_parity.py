@@ -1019,11 +1019,17 @@ def test_large_host_blocks(ecg, oracle, torch_cuda):
     assert np.array_equal(value, orig)  # the rebuilt slice is exact and its neighbour slices untouched
 
 
-def test_region_xor_batch(ecg, oracle, torch_cuda):
-    """ecg_region_xor_batch: galois_region_xor (dst ^= src) over S regions, any strides / sizes."""
+@pytest.mark.parametrize("aligned", [False, True])
+def test_region_xor_batch(ecg, oracle, torch_cuda, aligned):
+    """ecg_region_xor_batch: galois_region_xor (dst ^= src) over S regions, any strides / sizes
+    (16-byte-multiple strides go out as a strided launch, the others through a pointer table)."""
     torch = torch_cuda
-    for S, n in [(1, 1), (7, 1000), (64, 4096 + 3), (3, 1 << 20)]:
-        src = torch.randint(0, 256, (S, n + 16), dtype=torch.uint8, device="cuda")[:, 5:5 + n]  # odd stride/offset
+    for S, n in [(1, 1), (7, 1000), (64, 4096 + 3), (3, 1 << 20), (8, 4096), (5, 65536 + 32)]:
+        if aligned:
+            n = (n + 15) & ~15
+            src = torch.randint(0, 256, (S, n), dtype=torch.uint8, device="cuda")
+        else:
+            src = torch.randint(0, 256, (S, n + 16), dtype=torch.uint8, device="cuda")[:, 5:5 + n]  # odd stride/offset
         dst = torch.randint(0, 256, (S, n), dtype=torch.uint8, device="cuda")
         expect = (src.cpu().numpy() ^ dst.cpu().numpy())
         ecg.region_xor_batch(src, dst)
