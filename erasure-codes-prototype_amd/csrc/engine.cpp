@@ -6,7 +6,6 @@
 #include <algorithm>
 #include <atomic>
 #include <numeric>
-#include <unordered_set>
 
 namespace ecg {
 
@@ -295,6 +294,56 @@ bool same_ops(const std::vector<LinearOp>& a, const std::vector<LinearOp>& b) {
     return true;
 }
 
+// Open-addressing set of block addresses for the flush's hazard check: a run of S recorded calls
+// puts S * (k + m) addresses through it, and node-based hashing made that check most of a flush.
+// Addresses are never null (validated at record time), so 0 marks an empty slot.
+class PtrSet {
+public:
+    void clear() {  // O(table): shrink a table a large run left behind before many small runs reuse it
+        if (slots_.size() > 4096 && count_ * 8 < slots_.size()) {
+            slots_.assign(1024, 0);
+            mask_ = 1023;
+        } else if (count_) {
+            std::fill(slots_.begin(), slots_.end(), (uintptr_t)0);
+        }
+        count_ = 0;
+    }
+    bool contains(const void* ptr) const {
+        if (slots_.empty()) return false;
+        const uintptr_t p = (uintptr_t)ptr;
+        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
+            if (slots_[i] == p) return true;
+            if (slots_[i] == 0) return false;
+        }
+    }
+    void insert(const void* ptr) {
+        if ((count_ + 1) * 2 > slots_.size()) grow();
+        const uintptr_t p = (uintptr_t)ptr;
+        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
+            if (slots_[i] == p) return;
+            if (slots_[i] == 0) {
+                slots_[i] = p;
+                count_++;
+                return;
+            }
+        }
+    }
+
+private:
+    static size_t hash(uintptr_t p) { return (size_t)(((unsigned long long)p >> 4) * 0x9E3779B97F4A7C15ull >> 17); }
+    void grow() {
+        std::vector<uintptr_t> old;
+        old.swap(slots_);
+        slots_.assign(old.empty() ? 1024 : old.size() * 2, 0);
+        mask_ = slots_.size() - 1;
+        count_ = 0;
+        for (uintptr_t p : old)
+            if (p) insert((const void*)p);
+    }
+    std::vector<uintptr_t> slots_;
+    size_t mask_ = 0, count_ = 0;
+};
+
 // Pointer tables for pointer-table launches: a per-device ring of pinned host + device slots shared by
 // all threads (process lifetime, so no per-thread leak), each slot locked while it is filled and its
 // launch enqueued, and reused only after that launch has completed (its event).
@@ -377,16 +426,18 @@ int batch_flush() {
     q.swap(d.q);
     int rc = ECG_OK;
     size_t i = 0;
+    PtrSet wr, rd;
     while (i < q.size() && rc == ECG_OK) {
         // run [i, j): same engine / stream / B / plan, and no block written by one call and touched by another
-        std::unordered_set<const uint8_t*> wr, rd;
+        wr.clear();
+        rd.clear();
         auto touch = [&](const DeferredCall& c, bool check) {
             for (const LinearOp& op : *c.ops) {
                 for (int id : op.src_ids) {
-                    if (check && wr.count(c.blocks[id])) return false;
+                    if (check && wr.contains(c.blocks[id])) return false;
                 }
                 for (int id : op.dst_ids) {
-                    if (check && (wr.count(c.blocks[id]) || rd.count(c.blocks[id]))) return false;
+                    if (check && (wr.contains(c.blocks[id]) || rd.contains(c.blocks[id]))) return false;
                 }
             }
             for (const LinearOp& op : *c.ops) {
