@@ -178,10 +178,38 @@ static void decode_plans() {
     }
 }
 
+// Deferred-batch scope bookkeeping (record, hazard-split runs, strided-run detection) over fake device
+// addresses.  Only where no GPU exists: the flush then stops at its first launch with ECG_EHIP, after
+// every run has been formed; with a GPU the fake addresses would be launched.
+static void batch_scope() {
+    if (ecg_device_count() > 0) return;
+    ecg_coding_parameters cp{};
+    cp.k = 6;
+    cp.m = 3;
+    ecg_ec* ec = ecg_ec_factory(ECG_RS, &cp);
+    ecg_ec_set_memory(ec, ECG_MEM_DEVICE, nullptr);
+    for (int trial = 0; trial < 40; trial++) {
+        const int S = rnd(1, 3000), n = 9;
+        const int pool = rnd(1, 4) == 1 ? S * n : S * n * 3;  // sometimes shared blocks: hazards split runs
+        std::vector<char*> ptrs((size_t)S * n);
+        for (int s = 0; s < S; s++)
+            for (int b = 0; b < n; b++) {
+                const size_t slot = rnd(0, 3) ? (size_t)s * n + b : (size_t)rnd(0, pool - 1);
+                ptrs[(size_t)s * n + b] = (char*)(uintptr_t)(0x100000000ULL + slot * 4096);
+            }
+        if (ecg_batch_begin() != 0) abort();
+        for (int s = 0; s < S; s++) ecg_ec_encode(ec, &ptrs[(size_t)s * n], &ptrs[(size_t)s * n + 6], 4096);
+        const int rc = ecg_batch_end();
+        if (rc != 0 && rc != ECG_EHIP) abort();
+    }
+    ecg_ec_destroy(ec);
+}
+
 int main() {
     matrices();
     facade();
     decode_plans();
+    batch_scope();
     printf("host fuzz done\n");
     return 0;
 }
