@@ -25,7 +25,10 @@ Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line
 
 Multi-GPU: one process per GPU (torch.distributed.run), stripes sharded per rank (ecg_dist), no
 data-path collective: rank 0's coding plan broadcast before the run, barrier + synchronize around the
-timed region, elapsed time max-reduced, per-rank parity checksums all-gathered.
+timed region, elapsed time max-reduced, per-rank parity checksums all-gathered.  `--gpus N` with N > 1
+outside a torch.distributed environment starts N fresh rank processes itself (torch.distributed.run as a
+child process, before anything touches the GPU), relays rank 0's JSON line and exits with the ranks'
+status; inside one, N must equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -37,9 +40,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "erasure-codes-prototype_amd"))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 
-import ecg  # noqa: E402
+import ecg  # noqa: E402  (loads libecg.so lazily, on first use)
 import ecg_dist as D  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
@@ -49,7 +52,8 @@ METRIC = "GiB/s encode + single-block decode (device-resident), RS(10,4) 1 MiB b
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks (default: WORLD_SIZE under torch.distributed.run, else 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs-encode-decode",
@@ -60,7 +64,41 @@ def parse():
     ap.add_argument("--chunk", type=int, default=None, help="lrc-repair-ring: stripes per transfer")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rank bookkeeping only (gloo, no GPU): each rank reports itself, rank 0 prints one line")
     return ap.parse_args()
+
+
+def launch_ranks(a) -> int:
+    """`--gpus N` (N > 1) without a torch.distributed environment: start N fresh rank processes with
+    torch.distributed.run as a CHILD process (this process never touches the GPU and never exec()s),
+    forward their output, relay rank 0's JSON line on stdout, and return non-zero if any rank failed or
+    rank 0 printed no line.  Each rank re-runs this file with the same arguments; it sees WORLD_SIZE = N."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    lines = []
+    for ln in p.stdout:
+        if ln.startswith("{"):
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc != 0:
+        print(f"bench.py: {a.gpus} ranks under torch.distributed.run exited with status {rc}", file=sys.stderr)
+        return rc
+    if len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    print(lines[0], flush=True)
+    return 0
 
 
 def events(n):
@@ -94,14 +132,40 @@ def pmc_traffic(tag, workload_key):
 
 # ------------------------------------------------------------------------------- CPU baseline
 
+def host_cpus():
+    """The host CPUs this process may actually use: its affinity set, capped by the cgroup CPU quota
+    (cgroup v2 cpu.max "quota period"; the GPU box's job cgroup grants 16 CPUs of a 256-CPU machine, so
+    threads beyond the quota only time-slice).  Returns (threads, facts) with the facts stated in the line."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    threads = affinity if quota is None else max(1, min(affinity, int(quota + 0.999)))
+    return threads, {"cpu_model": model, "machine_cpus": os.cpu_count(), "affinity_cpus": affinity,
+                     "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(k, m, B, target_s):
     """Oracle CPU restatement (Jerasure algorithm, gf-complete-style SPLIT(8,4) PSHUFB region multiply)
     of the same step on a bounded sample: encode + single-erasure decode of S_cpu stripes, one
-    jerasure call per stripe, threads = min(16, cpu_count)."""
+    jerasure call per stripe (proxy.cpp:342-349), one worker thread per host CPU this process may use
+    (host_cpus: affinity capped by the cgroup quota)."""
     import numpy as np
     from oracle import ref
     ref.build()
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, facts = host_cpus()
     S = 4 * threads
     M = ref.reed_sol_vandermonde_coding_matrix(k, m)
     n = k + m
@@ -123,6 +187,8 @@ def cpu_baseline(k, m, B, target_s):
         reps += 1
     gib = reps * S * 2 * k * B / 2 ** 30
     return {"value": round(gib / t_total, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "threads_used": threads, "cores_available": threads,
+            "per_thread_GiBps": round(gib / t_total / threads, 3), **facts,
             "sample": f"{reps} x (encode + 1-erasure decode) of {S} RS({k},{m}) stripes x {B} B, "
                       f"one jerasure call per stripe, {threads} host threads, {t_total:.1f} s"}
 
@@ -535,10 +601,36 @@ def pc_merge(a, r):
 
 # ------------------------------------------------------------------------------- config 5
 
+def encode_waves(k, m, M, B, first, last, W, seed=0xEC0DE, on_wave=None):
+    """Encode global stripes [first, last) of the synthetic RS(k, m) batch in HBM-resident waves of at most
+    W stripes ([W][k+m][B] in one buffer).  Each wave's data is regenerated on device from the stripes'
+    global splitmix64 offsets (so a stripe's bytes do not depend on the sharding), encoded with ONE
+    ecg_encode_batch launch timed by HIP events, and folded into an order-independent parity checksum.
+    on_wave(s0, buf) may inspect a wave before the next one overwrites it.  Returns (seconds, checksum)."""
+    n = k + m
+    wave = torch.empty((min(W, max(1, last - first)), n, B), dtype=torch.uint8, device="cuda")
+    ev = events(1)[0]
+    kernel_s, checks = 0.0, 0
+    for s0 in range(first, last, W):
+        buf = wave[:min(W, last - s0)]
+        ecg.fill_random(buf, seed, word_offset=D.data_word_offset(s0, n, B))
+        ev[0].record()
+        ecg.encode_batch(k, m, M, buf[:, :k], buf[:, k:])
+        ev[1].record()
+        ev[1].synchronize()
+        kernel_s += ev[0].elapsed_time(ev[1]) / 1e3
+        checks = (checks + D.checksum64(buf[:, k:].contiguous())) & ((1 << 64) - 1)
+        if on_wave:
+            on_wave(s0, buf)
+    del wave
+    return kernel_s, checks
+
+
 def rs4m_waves(a, r):
     """RS(10,4), 4 MiB blocks, 65536 stripes sharded over the ranks; a rank's share (8192 stripes at N=8,
     448 GiB) exceeds HBM, so it is encoded in resident waves of 1024 stripes (56 GiB); each wave's input
-    is regenerated on device outside the timed region."""
+    is regenerated on device outside the timed region (tests/test_gpu_parity.py::test_config5_waves runs
+    the same code at a small size against the oracle)."""
     k, m = 10, 4
     n = k + m
     B = a.block_size or (4 << 20)
@@ -546,22 +638,9 @@ def rs4m_waves(a, r):
     W = 1024
     first, last = D.stripe_range(total, r)
     M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
-    wave = torch.empty((W, n, B), dtype=torch.uint8, device="cuda")
-    ev = events(1)[0]
-    kernel_s = 0.0
-    checks = 0
     D.barrier(r)
     torch.cuda.synchronize()
-    for s0 in range(first, last, W):
-        w = min(W, last - s0)
-        buf = wave[:w]
-        ecg.fill_random(buf, 0xEC0DE, word_offset=D.data_word_offset(s0, n, B))
-        ev[0].record()
-        ecg.encode_batch(k, m, M, buf[:, :k], buf[:, k:])
-        ev[1].record()
-        ev[1].synchronize()
-        kernel_s += ev[0].elapsed_time(ev[1]) / 1e3
-        checks = (checks + D.checksum64(buf[:, k:].contiguous())) & ((1 << 64) - 1)
+    kernel_s, checks = encode_waves(k, m, M, B, first, last, W)
     t_max = D.max_over_ranks(kernel_s, r, device="cuda")
     sums = D.gather_checksums(checks, r, device="cuda")
     data_bytes = total * k * B
@@ -627,9 +706,35 @@ def rs_host(a, r):
             "data": "synthetic (splitmix64 bytes generated on device, copied to pinned host buffers)"}
 
 
+def launch_check(a, r):
+    """--launch-check: the rank bookkeeping of a multi-GPU run without a GPU (gloo): every rank reports its
+    rank, local rank and pid; rank 0 prints them (tests/test_dist_cpu.py::test_bench_launcher)."""
+    D.init(r, "gloo")
+    me = [r.rank, r.local, os.getpid()]
+    if r.distributed:
+        t = torch.tensor(me, dtype=torch.int64)
+        out = [torch.zeros_like(t) for _ in range(r.world)]
+        torch.distributed.all_gather(out, t)
+        ranks = [x.tolist() for x in out]
+    else:
+        ranks = [me]
+    return {"metric": METRIC, "n_gpus": r.world, "launch_check": True, "ranks": ranks}
+
+
 def main():
     a = parse()
+    if a.gpus is not None and a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     r = D.from_env()
+    if a.gpus is not None and a.gpus != r.world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={r.world}")
+    if a.launch_check:
+        line = launch_check(a, r)
+        if r.rank == 0:
+            print(json.dumps(line), flush=True)
+        if r.distributed:
+            torch.distributed.destroy_process_group()
+        return
     # ECG_BENCH_SHARED_GPU=1: rehearsal of the N>1 path on a one-GPU box (every rank on cuda:0, gloo
     # for the bookkeeping collectives).  Exercises the rank logic only; its timings mean nothing.
     shared = os.environ.get("ECG_BENCH_SHARED_GPU") == "1"

@@ -307,6 +307,8 @@ int ecg_region_xor_batch(const void* d_src, long long src_stride, void* d_dst, l
     if (S < 0 || nbytes < 0) return ECG_EINVAL;
     if (S == 0 || nbytes == 0) return ECG_OK;
     if (!d_src || !d_dst) return ECG_EINVAL;
+    // recorded calls of an open batch scope go first (the pointer-table launch below does not flush)
+    if (const int rc = batch_flush_pending(); rc != ECG_OK) return rc;
     LinearOp op;
     op.src_ids = {0, 1};
     op.dst_ids = {1};
@@ -340,6 +342,7 @@ int ecg_perform_addition_batch(int block_num, int parity_num, const void* d_in, 
 int ecg_fill_random(void* d_dst, long long nbytes, unsigned long long seed, unsigned long long word_offset,
                     void* stream) {
     if (!d_dst || nbytes < 0) return ECG_EINVAL;
+    if (const int rc = batch_flush_pending(); rc != ECG_OK) return rc;
     hipError_t e = launch_fill_splitmix(d_dst, nbytes, seed, word_offset, (hipStream_t)stream);
     if (e != hipSuccess) {
         set_last_error(std::string("fill: ") + hipGetErrorString(e));

@@ -294,56 +294,6 @@ bool same_ops(const std::vector<LinearOp>& a, const std::vector<LinearOp>& b) {
     return true;
 }
 
-// Open-addressing set of block addresses for the flush's hazard check: a run of S recorded calls
-// puts S * (k + m) addresses through it, and node-based hashing made that check most of a flush.
-// Addresses are never null (validated at record time), so 0 marks an empty slot.
-class PtrSet {
-public:
-    void clear() {  // O(table): shrink a table a large run left behind before many small runs reuse it
-        if (slots_.size() > 4096 && count_ * 8 < slots_.size()) {
-            slots_.assign(1024, 0);
-            mask_ = 1023;
-        } else if (count_) {
-            std::fill(slots_.begin(), slots_.end(), (uintptr_t)0);
-        }
-        count_ = 0;
-    }
-    bool contains(const void* ptr) const {
-        if (slots_.empty()) return false;
-        const uintptr_t p = (uintptr_t)ptr;
-        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
-            if (slots_[i] == p) return true;
-            if (slots_[i] == 0) return false;
-        }
-    }
-    void insert(const void* ptr) {
-        if ((count_ + 1) * 2 > slots_.size()) grow();
-        const uintptr_t p = (uintptr_t)ptr;
-        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
-            if (slots_[i] == p) return;
-            if (slots_[i] == 0) {
-                slots_[i] = p;
-                count_++;
-                return;
-            }
-        }
-    }
-
-private:
-    static size_t hash(uintptr_t p) { return (size_t)(((unsigned long long)p >> 4) * 0x9E3779B97F4A7C15ull >> 17); }
-    void grow() {
-        std::vector<uintptr_t> old;
-        old.swap(slots_);
-        slots_.assign(old.empty() ? 1024 : old.size() * 2, 0);
-        mask_ = slots_.size() - 1;
-        count_ = 0;
-        for (uintptr_t p : old)
-            if (p) insert((const void*)p);
-    }
-    std::vector<uintptr_t> slots_;
-    size_t mask_ = 0, count_ = 0;
-};
-
 // Pointer tables for pointer-table launches: a per-device ring of pinned host + device slots shared by
 // all threads (process lifetime, so no per-thread leak), each slot locked while it is filled and its
 // launch enqueued, and reused only after that launch has completed (its event).
@@ -424,34 +374,36 @@ int batch_flush() {
     if (d.q.empty()) return ECG_OK;
     std::vector<DeferredCall> q;
     q.swap(d.q);
+    // runs [i, j): same engine / stream / B / plan, and no block written by one call and touched by another
+    auto same_run = [&](size_t i, size_t j) {
+        return q[j].eng == q[i].eng && q[j].st == q[i].st && q[j].B == q[i].B &&
+               (q[j].ops == q[i].ops || same_ops(*q[j].ops, *q[i].ops));
+    };
+    auto reads = [&](size_t c, auto&& f) {
+        for (const LinearOp& op : *q[c].ops)
+            for (int id : op.src_ids) f(q[c].blocks[id]);
+    };
+    auto writes = [&](size_t c, auto&& f) {
+        for (const LinearOp& op : *q[c].ops)
+            for (int id : op.dst_ids) f(q[c].blocks[id]);
+    };
+    const std::vector<size_t> ends = form_runs(q.size(), same_run, reads, writes);
+    int caller_dev = -1, cur_dev = -1;
+    (void)hipGetDevice(&caller_dev);
+    cur_dev = caller_dev;
     int rc = ECG_OK;
     size_t i = 0;
-    PtrSet wr, rd;
-    while (i < q.size() && rc == ECG_OK) {
-        // run [i, j): same engine / stream / B / plan, and no block written by one call and touched by another
-        wr.clear();
-        rd.clear();
-        auto touch = [&](const DeferredCall& c, bool check) {
-            for (const LinearOp& op : *c.ops) {
-                for (int id : op.src_ids) {
-                    if (check && wr.contains(c.blocks[id])) return false;
-                }
-                for (int id : op.dst_ids) {
-                    if (check && (wr.contains(c.blocks[id]) || rd.contains(c.blocks[id]))) return false;
-                }
-            }
-            for (const LinearOp& op : *c.ops) {
-                for (int id : op.src_ids) rd.insert(c.blocks[id]);
-                for (int id : op.dst_ids) wr.insert(c.blocks[id]);
-            }
-            return true;
-        };
-        touch(q[i], false);
-        size_t j = i + 1;
-        while (j < q.size() && q[j].eng == q[i].eng && q[j].st == q[i].st && q[j].B == q[i].B &&
-               (q[j].ops == q[i].ops || same_ops(*q[j].ops, *q[i].ops)) && touch(q[j], true))
-            j++;
+    for (size_t r = 0; r < ends.size() && rc == ECG_OK; r++) {
+        const size_t j = ends[r];
         Engine* eng = q[i].eng;
+        if (eng->device() != cur_dev) {  // a run launches on the device its calls were recorded on
+            if (hipSetDevice(eng->device()) != hipSuccess) {
+                set_last_error("batch flush: hipSetDevice failed");
+                rc = ECG_EHIP;
+                break;
+            }
+            cur_dev = eng->device();
+        }
         if (j - i == 1) {
             rc = eng->launch_direct(*q[i].ops, q[i].blocks.data(), q[i].B, q[i].st);
         } else {
@@ -471,8 +423,11 @@ int batch_flush() {
         }
         i = j;
     }
+    if (cur_dev != caller_dev && caller_dev >= 0) (void)hipSetDevice(caller_dev);
     return rc;
 }
+
+int batch_flush_pending() { return t_defer.q.empty() ? ECG_OK : batch_flush(); }
 
 int batch_end() {
     if (!t_defer.active) return ECG_EINVAL;

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -98,10 +99,99 @@ private:
 // batch, a pointer-table launch otherwise -- splitting a run where a call touches a block an earlier
 // call of the run writes (or writes one it reads).  Host-tier and batched calls flush first, so call
 // order is kept.
+// A flush launches each run on its engine's device (the calling thread's device is restored after).  If a
+// launch fails, the flush stops there and returns the error; the calls of that run and of every later
+// run are dropped (not retried by a later flush).
 int batch_begin();
 int batch_flush();
 int batch_end();
 bool batch_active();
+// Flush this thread's recorded calls, if any (entry points that launch directly call it first, so a
+// recorded call never runs after a later direct launch).
+int batch_flush_pending();
+
+// Open-addressing set of block addresses for the flush's hazard check: a run of S recorded calls puts
+// S * (k + m) addresses through it, and node-based hashing made that check most of a flush.  Addresses
+// are never null (validated at record time), so 0 marks an empty slot.
+class PtrSet {
+public:
+    void clear() {  // O(table): shrink a table a large run left behind before many small runs reuse it
+        if (slots_.size() > 4096 && count_ * 8 < slots_.size()) {
+            slots_.assign(1024, 0);
+            mask_ = 1023;
+        } else if (count_) {
+            std::fill(slots_.begin(), slots_.end(), (uintptr_t)0);
+        }
+        count_ = 0;
+    }
+    bool contains(const void* ptr) const {
+        if (slots_.empty()) return false;
+        const uintptr_t p = (uintptr_t)ptr;
+        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
+            if (slots_[i] == p) return true;
+            if (slots_[i] == 0) return false;
+        }
+    }
+    void insert(const void* ptr) {
+        if ((count_ + 1) * 2 > slots_.size()) grow();
+        const uintptr_t p = (uintptr_t)ptr;
+        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
+            if (slots_[i] == p) return;
+            if (slots_[i] == 0) {
+                slots_[i] = p;
+                count_++;
+                return;
+            }
+        }
+    }
+    size_t size() const { return count_; }
+
+private:
+    static size_t hash(uintptr_t p) { return (size_t)(((unsigned long long)p >> 4) * 0x9E3779B97F4A7C15ull >> 17); }
+    void grow() {
+        std::vector<uintptr_t> old;
+        old.swap(slots_);
+        slots_.assign(old.empty() ? 1024 : old.size() * 2, 0);
+        mask_ = slots_.size() - 1;
+        count_ = 0;
+        for (uintptr_t p : old)
+            if (p) insert((const void*)p);
+    }
+    std::vector<uintptr_t> slots_;
+    size_t mask_ = 0, count_ = 0;
+};
+
+// Run formation of the flush (pure host logic, no HIP; fuzzed against a quadratic check in
+// tests/sanitize/host_fuzz.cpp).  Splits calls [0, n) into maximal runs [i, j): every call of a run has
+// same_run(i, c) true, and no call reads or writes a block an earlier call of its run writes, or writes a
+// block an earlier call of its run reads.  reads(c, f) / writes(c, f) call f(address) for each block call
+// c reads / writes.  Returns the run ends (the last one is n).
+template <class SameRun, class Reads, class Writes>
+std::vector<size_t> form_runs(size_t n, SameRun same_run, Reads reads, Writes writes) {
+    std::vector<size_t> ends;
+    PtrSet wr, rd;
+    size_t i = 0;
+    while (i < n) {
+        wr.clear();
+        rd.clear();
+        auto add = [&](size_t c) {
+            reads(c, [&](const void* p) { rd.insert(p); });
+            writes(c, [&](const void* p) { wr.insert(p); });
+        };
+        add(i);
+        size_t j = i + 1;
+        for (; j < n && same_run(i, j); j++) {
+            bool clash = false;
+            reads(j, [&](const void* p) { clash = clash || wr.contains(p); });
+            writes(j, [&](const void* p) { clash = clash || wr.contains(p) || rd.contains(p); });
+            if (clash) break;
+            add(j);
+        }
+        ends.push_back(j);
+        i = j;
+    }
+    return ends;
+}
 
 // Last HIP error seen by this thread (for diagnostics through the C ABI).
 const char* last_error_string();

@@ -13,9 +13,11 @@
 //   * straight-line code (no per-coefficient branches); matrices whose entries are all 0/1
 //     (perform_addition, LRC local rows, PC merges) take a BINARY flavour: one v_bitop3
 //     acc ^ (x & mask) per coefficient-dword.
-//   * grid: one 256-thread workgroup per 4 KiB chunk of every block of a stripe (cols_per_wg = 256),
-//     workgroups mapped XCD-contiguously (grid_map 1), non-temporal loads and stores -- measured
-//     best on MI355X (profiles/r01/microbench.*: 6.1 TB/s encode vs 5.3 TB/s for 16 KiB chunks).
+//   * grid: one kThreads = 128-thread workgroup (2 waves) per 2 KiB chunk of every block of a stripe
+//     (cols_per_wg = kThreads 16-byte columns), the workgroup -> chunk map chosen per launch (grid_map
+//     auto: XCD-contiguous when the outputs live in the input stripes, stripe-per-XCD otherwise),
+//     non-temporal loads and stores -- measured best on MI355X (profiles/r01/microbench.*: 16 KiB chunks
+//     5.35 TB/s -> 4 KiB 5.80 -> XCD map 6.14 -> 128 threads / 2 KiB + auto map 6.28-6.33 TB/s).
 // VALU cost per 16-byte column: 20 ops to split one input, ~18 per coefficient (GENERAL) or 4
 // (BINARY); for RS(10,4) encode ~1000 ops per 160 data bytes, ~35 % of gfx950's integer issue rate
 // at the HBM roofline.

@@ -121,7 +121,10 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
  * otherwise.  Outputs are defined once the flush's work completes on the stream.  A run is split
  * where a call reads or writes a block an earlier call of the run writes, or writes one it reads
  * (blocks compared by address: partially overlapping blocks are not allowed).  Host-tier and batched
- * calls made inside the scope flush first.  Scopes do not nest (ECG_EINVAL). */
+ * calls made inside the scope (ecg_region_xor_batch and ecg_fill_random included) flush first.  A run
+ * launches on the device its calls were recorded on, whatever the thread's device at flush time.  If a
+ * launch fails, the flush returns its error and the calls of that run and of all later runs are
+ * discarded (the scope stays open, empty).  Scopes do not nest (ECG_EINVAL). */
 int ecg_batch_begin(void);
 int ecg_batch_flush(void);
 int ecg_batch_end(void);

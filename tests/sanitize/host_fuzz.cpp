@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "ecg.h"
+#include "engine.hpp"  // ecg::form_runs, ecg::PtrSet (pure host logic of the batch-scope flush)
 
 static std::mt19937_64 rng(12345);
 static int rnd(int lo, int hi) { return std::uniform_int_distribution<int>(lo, hi)(rng); }
@@ -178,9 +179,73 @@ static void decode_plans() {
     }
 }
 
+// Run formation of the batch-scope flush (ecg::form_runs) against a quadratic restatement of its rule,
+// over many runs per flush so PtrSet's clear / shrink / grow paths all execute under the sanitizers.
+static void run_formation() {
+    struct Call {
+        int plan;
+        std::vector<const void*> rd, wr;
+    };
+    long long runs_seen = 0;
+    for (int trial = 0; trial < 400; trial++) {
+        const int n = rnd(1, trial % 10 == 0 ? 6000 : 300);
+        const int plans = rnd(1, 3);
+        // pool: addresses shared between calls (hazards) or mostly private (long runs, big tables)
+        const int pool = rnd(0, 2) ? n * 12 : rnd(2, 40);
+        std::vector<Call> c(n);
+        for (auto& x : c) {
+            x.plan = rnd(0, plans - 1) * (rnd(0, 9) == 0 ? 1 : 0);
+            const int nr = rnd(0, 5), nw = rnd(1, 3);
+            for (int i = 0; i < nr; i++) x.rd.push_back((const void*)(uintptr_t)(0x1000 + 16 * rnd(0, pool)));
+            for (int i = 0; i < nw; i++) x.wr.push_back((const void*)(uintptr_t)(0x1000 + 16 * rnd(0, pool)));
+        }
+        auto same = [&](size_t i, size_t j) { return c[i].plan == c[j].plan; };
+        auto reads = [&](size_t i, auto&& f) { for (auto p : c[i].rd) f(p); };
+        auto writes = [&](size_t i, auto&& f) { for (auto p : c[i].wr) f(p); };
+        const std::vector<size_t> ends = ecg::form_runs((size_t)n, same, reads, writes);
+        // quadratic reference: extend while the plan matches and no earlier call of the run conflicts
+        size_t i = 0, r = 0;
+        while (i < (size_t)n) {
+            size_t j = i + 1;
+            for (; j < (size_t)n && c[j].plan == c[i].plan; j++) {
+                bool clash = false;
+                for (size_t e = i; e < j && !clash; e++) {
+                    for (auto p : c[j].rd) clash |= std::count(c[e].wr.begin(), c[e].wr.end(), p) > 0;
+                    for (auto p : c[j].wr)
+                        clash |= std::count(c[e].wr.begin(), c[e].wr.end(), p) + std::count(c[e].rd.begin(), c[e].rd.end(), p) > 0;
+                }
+                if (clash) break;
+            }
+            if (r >= ends.size() || ends[r] != j) {
+                fprintf(stderr, "form_runs mismatch: trial %d run %zu\n", trial, r);
+                abort();
+            }
+            i = j;
+            r++;
+        }
+        if (r != ends.size()) abort();
+        runs_seen += (long long)r;
+    }
+    // PtrSet alone: grow past 1024 slots, shrink on clear, duplicates, membership after regrowth
+    ecg::PtrSet s;
+    for (int round = 0; round < 6; round++) {
+        const int cnt = round % 2 ? 20000 : 7;
+        for (int i = 1; i <= cnt; i++) s.insert((const void*)(uintptr_t)(i * 48));
+        for (int i = 1; i <= cnt; i++) s.insert((const void*)(uintptr_t)(i * 48));
+        if (s.size() != (size_t)cnt) abort();
+        for (int i = 1; i <= cnt; i++)
+            if (!s.contains((const void*)(uintptr_t)(i * 48))) abort();
+        if (s.contains((const void*)(uintptr_t)(cnt * 48 + 48))) abort();
+        s.clear();
+        if (s.size() != 0 || s.contains((const void*)(uintptr_t)48)) abort();
+    }
+    printf("run formation: %lld runs checked\n", runs_seen);
+}
+
 // Deferred-batch scope bookkeeping (record, hazard-split runs, strided-run detection) over fake device
-// addresses.  Only where no GPU exists: the flush then stops at its first launch with ECG_EHIP, after
-// every run has been formed; with a GPU the fake addresses would be launched.
+// addresses.  Only where no GPU exists: the flush then stops at its first launch with ECG_EHIP (a
+// program-table allocation), so only the first run is launched; the run boundaries of every flush are
+// covered by run_formation() above.  With a GPU the fake addresses would be launched.
 static void batch_scope() {
     if (ecg_device_count() > 0) return;
     ecg_coding_parameters cp{};
@@ -209,6 +274,7 @@ int main() {
     matrices();
     facade();
     decode_plans();
+    run_formation();
     batch_scope();
     printf("host fuzz done\n");
     return 0;

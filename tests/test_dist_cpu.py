@@ -184,3 +184,33 @@ def test_ring_exchange_single_rank_and_shape_checks():
         D.ring_exchange(a.t(), torch.zeros(4, 3, dtype=torch.uint8), r)
     with pytest.raises(ValueError):
         D.pipelined_ring_repair(3, 0, None, None, a, b, r)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_launcher_spawns_ranks(n):
+    """`python bench.py --gpus N` outside torch.distributed starts N fresh rank processes itself (the
+    driver's SCALE command) and relays rank 0's line with n_gpus = N.  --launch-check stops every rank
+    after the gloo bookkeeping, before any GPU call."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--launch-check"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == n
+    ranks = line["ranks"]
+    assert sorted(r[0] for r in ranks) == list(range(n)) and sorted(r[1] for r in ranks) == list(range(n))
+    assert len({r[2] for r in ranks}) == n and os.getpid() not in {r[2] for r in ranks}  # fresh processes
+
+
+def test_bench_gpus_must_match_world():
+    """Inside torch.distributed, --gpus N must equal WORLD_SIZE (a mismatched line would misreport n_gpus)."""
+    import subprocess
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr

@@ -591,6 +591,44 @@ def test_full_size_rs10_4_round_trip(ecg, oracle, torch_cuda):
     torch.cuda.empty_cache()
 
 
+def test_config5_waves_sharded(ecg, oracle, torch_cuda):
+    """BASELINE config 5 (RS(10,4), 4 MiB blocks, a stripe batch sharded over GPUs and encoded in
+    HBM-resident waves) through bench.py's own encode_waves at a small size: 67 stripes, waves of 32.
+    Sampled stripes (first / last of a wave, both shard edges) are compared byte for byte with the oracle
+    on host-generated data, and the per-rank parity checksums of a 2-way and a 3-way split, combined,
+    equal the unsplit checksum (the SCALE run's bit-exact verdict)."""
+    torch = torch_cuda
+    import ecg_dist as D
+    from bench import encode_waves
+    k, m, B, total, W = 10, 4, 4 << 20, 67, 32
+    n = k + m
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    sample = {0, 31, 32, 33, 34, 44, 45, 66}
+    checked = set()
+
+    def check(s0, buf):
+        for s in range(s0, s0 + buf.shape[0]):
+            if s not in sample or s in checked:
+                continue
+            h = buf[s - s0].cpu().numpy()
+            data = [oracle.splitmix_bytes(0xEC0DE, (s * n + j) * B // 8, B) for j in range(k)]
+            assert same([h[j] for j in range(k)], data), f"stripe {s}: device data != host splitmix"
+            ref = [np.zeros(B, np.uint8) for _ in range(m)]
+            oracle.jerasure_matrix_encode_simd(k, m, M, data, ref, B)
+            assert same([h[k + i] for i in range(m)], ref), f"stripe {s}: parity mismatch"
+            checked.add(s)
+
+    _, whole = encode_waves(k, m, M, B, 0, total, W, on_wave=check)
+    assert checked == sample
+    for world in (2, 3):
+        parts = []
+        for rank in range(world):
+            first, last = D.stripe_range(total, D.Rank(rank, world, rank))
+            parts.append(encode_waves(k, m, M, B, first, last, W)[1])
+        assert D.combine(parts) == whole, world
+    torch.cuda.empty_cache()
+
+
 def test_matrix_apply_multi_with_stripe_subset(ecg, oracle, torch_cuda):
     """Several programs per launch + launch over a subset of the batch (stripe_of indirection)."""
     torch = torch_cuda
@@ -898,6 +936,68 @@ def test_batch_scope_hazards_split_runs(ecg, torch_cuda):
         with pytest.raises(ecg.EcgError):
             ecg.batch().__enter__()  # scopes do not nest
     assert (h_dst == 6).all()
+
+
+def test_batch_scope_then_direct_batched_calls(ecg, oracle, torch_cuda):
+    """Batched entry points that launch directly flush the scope's recorded calls first, whatever launch
+    they pick: region_xor_batch with S = 1 and with unaligned strides (pointer-table launch), and
+    fill_random.  Without the flush they would run before the recorded encode they depend on."""
+    torch = torch_cuda
+    k, m, B = 4, 2, 4096
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
+    st = torch.empty((3, k + m, B + 4), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, 77)
+    host = st.cpu().numpy()
+    want = []
+    for s in range(3):
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode(k, m, M, [host[s, j, :B].copy() for j in range(k)], ref, B)
+        want.append(ref)
+    acc = torch.zeros((B,), dtype=torch.uint8, device="cuda")
+    with ecg.batch():
+        ec.encode([st[0, j, :B] for j in range(k)], [st[0, k + i, :B] for i in range(m)], B)
+        ecg.region_xor_batch(st[0, k, :B].reshape(1, B), acc.reshape(1, B))  # S = 1: pointer-table launch
+    torch.cuda.synchronize()
+    assert np.array_equal(acc.cpu().numpy(), want[0][0])
+    # unaligned strides (B + 4): not a strided launch either
+    acc2 = torch.zeros((2, B + 4), dtype=torch.uint8, device="cuda")
+    with ecg.batch():
+        for s in (1, 2):
+            ec.encode([st[s, j, :B] for j in range(k)], [st[s, k + i, :B] for i in range(m)], B)
+        ecg.region_xor_batch(st[1:, k + 1, :B], acc2[:, :B])
+    torch.cuda.synchronize()
+    for s in (1, 2):
+        assert np.array_equal(acc2[s - 1, :B].cpu().numpy(), want[s][1]), s
+    # fill_random after a recorded encode that reads the filled block: the encode sees the old bytes
+    blk = torch.empty((k + m, B), dtype=torch.uint8, device="cuda")
+    blk[:k].copy_(st[0, :k, :B])
+    with ecg.batch():
+        ec.encode([blk[j] for j in range(k)], [blk[k + i] for i in range(m)], B)
+        ecg.fill_random(blk[0], 99)
+    torch.cuda.synchronize()
+    assert same([blk[k + i].cpu().numpy() for i in range(m)], want[0])
+
+
+def test_batch_scope_flush_on_recording_device(ecg, torch_cuda):
+    """Calls recorded on device 0 and flushed after the thread switched to device 1 launch on device 0
+    (needs two GPUs; the pool's boxes have one)."""
+    torch = torch_cuda
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=4, m=2))
+    a = torch.randint(0, 256, (6, 4096), dtype=torch.uint8, device="cuda:0")
+    ref = a.clone()
+    ecg.encode_batch(4, 2, ecg.reed_sol_vandermonde_coding_matrix(4, 2), ref[None, :4], ref[None, 4:])
+    a[4:] = 0
+    torch.cuda.set_device(0)
+    ecg.lib().ecg_set_device(0)
+    with ecg.batch():
+        ec.encode([a[j] for j in range(4)], [a[4 + i] for i in range(2)], 4096)
+        ecg.lib().ecg_set_device(1)
+    ecg.lib().ecg_set_device(0)
+    torch.cuda.synchronize(0)
+    assert torch.equal(a, ref)
 
 
 # ------------------------------------------------------------------ randomized code parameters, every family
