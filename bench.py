@@ -251,6 +251,9 @@ def rs_encode_decode(a, r):
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": pmc_traffic("encode", f"rs{k}{m}_B{B}_S{S}"),
+                     "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE "
+                                       "passes of this bench command (FETCH x2, KiB -> B, per launch), committed "
+                                       "with the round's profiles; not measured inside this run",
                      "algorithmic_bytes_per_launch": enc_bytes,
                      "decode_achieved": round(dec_bytes / dec_avg / 1e9, 1),
                      "decode_frac": round(dec_bytes / dec_avg / 1e9 / HBM_PEAK_GBS, 4),

@@ -1280,22 +1280,26 @@ def test_decode_duplicate_erasures(ecg, oracle, torch_cuda):
         assert same([x.cpu().numpy() for x in dev], A), er  # undecodable: nothing written, as in the library
 
 
-@pytest.mark.parametrize("layout", ["strided", "scattered"])
+@pytest.mark.parametrize("layout", ["strided", "scattered", "unaligned"])
 def test_batch_scope_layouts(ecg, oracle, torch_cuda, layout):
     """A batch-scope run whose blocks form one strided batch goes out as a strided launch; scattered
-    blocks (random offsets in a pool) as a pointer-table launch.  Both give the oracle's bytes, for
-    encode and for a decode plan of several ops."""
-    torch = torch_cuda
+    blocks (random offsets in a pool) as a pointer-table launch; unaligned scattered blocks as a
+    pointer-table launch of the byte kernel.  All give the oracle's bytes, for encode and for a decode
+    plan of several ops."""
+    _batch_scope_layouts(ecg, oracle, torch_cuda, layout)
+
+
+def _batch_scope_layouts(ecg, oracle, torch, layout):
     k, m, S, B = 6, 3, 24, 8192 + 16
     n = k + m
     M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
-    pool = torch.empty(((S * n + 7) * B,), dtype=torch.uint8, device="cuda")
+    pool = torch.empty(((S * n + 7) * B + 16,), dtype=torch.uint8, device="cuda")
     if layout == "strided":
         offs = [[(s * n + b) * B for b in range(n)] for s in range(S)]
     else:
         slots = list(range(S * n + 7))
         random.Random(4).shuffle(slots)
-        offs = [[slots[s * n + b] * B for b in range(n)] for s in range(S)]
+        offs = [[slots[s * n + b] * B + (3 if layout == "unaligned" else 0) for b in range(n)] for s in range(S)]
     host = [[rnd(B, 1000 + s * n + b) for b in range(k)] for s in range(S)]
     blk = [[pool[o:o + B] for o in offs[s]] for s in range(S)]
     for s in range(S):
