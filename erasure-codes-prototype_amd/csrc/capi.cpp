@@ -62,6 +62,15 @@ int ecg_host_contexts(void) { return Engine::instance().host_contexts(); }
 int ecg_batch_begin(void) { return batch_begin(); }
 int ecg_batch_flush(void) { return batch_flush(); }
 int ecg_batch_end(void) { return batch_end(); }
+int ecg_batch_scratch(const void* ptr, size_t bytes) { return batch_scratch(ptr, bytes); }
+int ecg_batch_last_stats(long long* recorded, long long* composed, long long* launches, long long* materialised) {
+    const FlushStats s = last_flush_stats();
+    if (recorded) *recorded = s.recorded;
+    if (composed) *composed = s.composed;
+    if (launches) *launches = s.launches;
+    if (materialised) *materialised = s.materialised;
+    return ECG_OK;
+}
 
 int ecg_set_option(int option, long long value) { return set_option(option, value) == 0 ? ECG_OK : ECG_EINVAL; }
 long long ecg_get_option(int option) { return get_option(option); }

@@ -5,7 +5,12 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
+#include <map>
 #include <numeric>
+#include <tuple>
+
+#include "gf256.hpp"
 
 namespace ecg {
 
@@ -271,17 +276,11 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
 
 namespace {
 
-struct DeferredCall {
-    Engine* eng;
-    hipStream_t st;
-    long long B;
-    std::shared_ptr<const std::vector<LinearOp>> ops;  // shared by consecutive calls with the same plan
-    std::vector<uint8_t*> blocks;                      // the call's block space (device pointers)
-};
-
 struct DeferScope {
     bool active = false;
     std::vector<DeferredCall> q;
+    ScratchRanges scratch;
+    FlushStats stats;
 };
 
 thread_local DeferScope t_defer;
@@ -366,19 +365,323 @@ int batch_begin() {
     if (t_defer.active) return ECG_EINVAL;  // scopes do not nest
     t_defer.active = true;
     t_defer.q.clear();
+    t_defer.scratch.clear();
     return ECG_OK;
 }
+
+int batch_scratch(const void* p, size_t bytes) {
+    if (!t_defer.active || !p) return ECG_EINVAL;
+    if (bytes == 0) return ECG_OK;
+    if ((uintptr_t)p + bytes < (uintptr_t)p) return ECG_EINVAL;
+    t_defer.scratch.add((uintptr_t)p, (uintptr_t)p + bytes);
+    return ECG_OK;
+}
+
+FlushStats last_flush_stats() { return t_defer.stats; }
+
+// ScratchRanges: sorted disjoint [lo, hi); add() merges overlapping and touching ranges.
+void ScratchRanges::add(uintptr_t lo, uintptr_t hi) {
+    auto it = std::lower_bound(r_.begin(), r_.end(), std::make_pair(lo, (uintptr_t)0));
+    if (it != r_.begin() && std::prev(it)->second >= lo) --it;
+    auto e = it;
+    while (e != r_.end() && e->first <= hi) {
+        lo = std::min(lo, e->first);
+        hi = std::max(hi, e->second);
+        ++e;
+    }
+    it = r_.erase(it, e);
+    r_.insert(it, {lo, hi});
+}
+
+bool ScratchRanges::holds(const void* p, long long B) const {
+    const uintptr_t a = (uintptr_t)p;
+    auto it = std::upper_bound(r_.begin(), r_.end(), std::make_pair(a, UINTPTR_MAX));
+    if (it == r_.begin()) return false;
+    --it;
+    return a >= it->first && a + (uintptr_t)B <= it->second;
+}
+
+namespace {
+
+// A linear combination of real blocks over GF(2^8): (block, coefficient) terms, coefficients != 0 once
+// normalised.  Small (a partial repair combines <= k' blocks), so a flat vector.
+using Terms = std::vector<std::pair<uint8_t*, uint8_t>>;
+
+void add_term(Terms& t, uint8_t* p, int c) {
+    if (!c) return;
+    for (auto& x : t)
+        if (x.first == p) {
+            x.second ^= (uint8_t)c;
+            return;
+        }
+    t.emplace_back(p, (uint8_t)c);
+}
+
+void drop_zero_terms(Terms& t) {
+    t.erase(std::remove_if(t.begin(), t.end(), [](const std::pair<uint8_t*, uint8_t>& x) { return x.second == 0; }),
+            t.end());
+}
+
+struct Expr {
+    Engine* eng;
+    hipStream_t st;
+    long long B;
+    Terms t;
+};
+
+// One composed call writing rows[i].first = rows[i].second: inputs in first-appearance order (the same
+// for every stripe of one call pattern, so equal patterns intern to one plan), rows that combine to
+// nothing become a k_in = 0 op (zero bytes, what the sequential calls leave there).
+DeferredCall make_call(Engine* eng, hipStream_t st, long long B, const std::vector<std::pair<uint8_t*, Terms>>& rows) {
+    DeferredCall c{eng, st, B, nullptr, {}};
+    // a block written twice by one op holds its last row (every row reads before any row writes)
+    std::vector<bool> keep(rows.size(), true);
+    for (size_t i = 0; i < rows.size(); i++)
+        for (size_t j = i + 1; j < rows.size() && keep[i]; j++)
+            if (rows[j].first == rows[i].first) keep[i] = false;
+    std::vector<uint8_t*> ins;
+    for (size_t i = 0; i < rows.size(); i++) {
+        if (!keep[i]) continue;
+        const auto& r = rows[i];
+        for (auto& x : r.second)
+            if (std::find(ins.begin(), ins.end(), x.first) == ins.end()) ins.push_back(x.first);
+    }
+    const int n = (int)ins.size();
+    auto ops = std::make_shared<std::vector<LinearOp>>();
+    LinearOp full, zero;
+    for (int j = 0; j < n; j++) full.src_ids.push_back(j);
+    c.blocks = ins;
+    for (size_t i = 0; i < rows.size(); i++) {
+        if (!keep[i]) continue;
+        const auto& r = rows[i];
+        const int id = (int)c.blocks.size();
+        c.blocks.push_back(r.first);
+        if (r.second.empty()) {
+            zero.dst_ids.push_back(id);
+            continue;
+        }
+        full.dst_ids.push_back(id);
+        const size_t base = full.coef.size();
+        full.coef.resize(base + (size_t)n, 0);
+        for (auto& x : r.second)
+            full.coef[base + (size_t)(std::find(ins.begin(), ins.end(), x.first) - ins.begin())] = x.second;
+    }
+    if (full.m_out() > 0) ops->push_back(std::move(full));
+    if (zero.m_out() > 0) ops->push_back(std::move(zero));
+    c.ops = std::move(ops);
+    return c;
+}
+
+}  // namespace
+
+std::vector<DeferredCall> compose_scratch(std::vector<DeferredCall>&& q, const ScratchRanges& scratch, bool scope_end,
+                                          long long* materialised) {
+    std::vector<DeferredCall> out;
+    out.reserve(q.size());
+    std::unordered_map<uint8_t*, Expr> ex;                     // scratch block -> what it holds
+    std::unordered_map<uint8_t*, std::vector<uint8_t*>> users;  // real block -> scratch blocks whose expr reads it
+    long long nmat = 0;
+    // While a call's writes are processed, expressions written out because the call overwrites a block
+    // they read join the call's own op (`collect`): one op reads every input before it writes any
+    // output, so neither side sees the other's writes (a separate earlier call writing scratch block s
+    // would clobber an s the op itself still reads).
+    std::vector<std::pair<uint8_t*, Terms>>* collect = nullptr;
+    Engine* collect_eng = nullptr;
+    long long collect_B = 0;
+    std::function<void(uint8_t*)> before_write;
+    auto materialise = [&](uint8_t* s) {
+        auto it = ex.find(s);
+        if (it == ex.end()) return;
+        Expr e = std::move(it->second);
+        ex.erase(it);
+        before_write(s);
+        if (collect && e.eng == collect_eng && e.B == collect_B) collect->emplace_back(s, std::move(e.t));
+        else out.push_back(make_call(e.eng, e.st, e.B, {{s, std::move(e.t)}}));
+        nmat++;
+    };
+    // Top level: write the expressions of `ss` out, with every expression they drag along, as ONE op
+    // (expressions can read each other's real blocks both ways once a scratch block's expression read
+    // its own old contents, so written one by one the second would read the first's new bytes).
+    auto write_out = [&](const std::vector<uint8_t*>& ss) {
+        std::vector<std::pair<uint8_t*, Terms>> rows;
+        Engine* eng = nullptr;
+        hipStream_t st = nullptr;
+        long long B = 0;
+        for (uint8_t* s : ss) {
+            auto it = ex.find(s);
+            if (it == ex.end()) continue;
+            if (!collect) {
+                eng = collect_eng = it->second.eng;
+                st = it->second.st;
+                B = collect_B = it->second.B;
+                collect = &rows;
+            }
+            materialise(s);
+        }
+        collect = nullptr;
+        if (!rows.empty()) out.push_back(make_call(eng, st, B, rows));
+    };
+    // d is about to be overwritten: every expression still reading d is written out first
+    before_write = [&](uint8_t* d) {
+        auto u = users.find(d);
+        if (u == users.end()) return;
+        std::vector<uint8_t*> v = std::move(u->second);
+        users.erase(u);
+        for (uint8_t* s : v) {
+            auto it = ex.find(s);
+            if (it == ex.end()) continue;
+            for (auto& x : it->second.t)
+                if (x.first == d) {
+                    materialise(s);
+                    break;
+                }
+        }
+    };
+    for (DeferredCall& c : q) {
+        bool touches = false;
+        for (const LinearOp& op : *c.ops) {
+            for (int id : op.src_ids) touches = touches || ex.count(c.blocks[id]);
+            for (int id : op.dst_ids) touches = touches || scratch.holds(c.blocks[id], c.B);
+        }
+        if (!touches) {
+            // expressions reading blocks this call overwrites go out first, together as one op
+            std::vector<std::pair<uint8_t*, Terms>> rows;
+            if (!users.empty()) {
+                collect = &rows;
+                collect_eng = c.eng;
+                collect_B = c.B;
+                for (const LinearOp& op : *c.ops)
+                    for (int id : op.dst_ids) before_write(c.blocks[id]);
+                collect = nullptr;
+            }
+            if (!rows.empty()) out.push_back(make_call(c.eng, c.st, c.B, rows));
+            out.push_back(std::move(c));
+            continue;
+        }
+        for (const LinearOp& op : *c.ops) {
+            const int k = op.k_in(), m = op.m_out();
+            // inputs whose expression was recorded on another stream / device / block size are written
+            // for real first -- before any row is built, since writing them out can overwrite blocks
+            // other expressions (and so the rows) read
+            std::vector<uint8_t*> foreign;
+            for (int id : op.src_ids) {
+                auto it = ex.find(c.blocks[id]);
+                if (it != ex.end() && !(it->second.eng == c.eng && it->second.st == c.st && it->second.B == c.B))
+                    foreign.push_back(c.blocks[id]);
+            }
+            if (!foreign.empty()) write_out(foreign);
+            std::vector<std::pair<uint8_t*, Terms>> rows((size_t)m);
+            for (int p = 0; p < m; p++) {
+                Terms& t = rows[p].second;
+                for (int j = 0; j < k; j++) {
+                    const int cf = op.coef[(size_t)p * k + j];
+                    if (!cf) continue;
+                    uint8_t* src = c.blocks[op.src_ids[j]];
+                    auto it = ex.find(src);
+                    if (it != ex.end()) {
+                        for (auto& x : it->second.t) add_term(t, x.first, gf::mul(cf, x.second));
+                        continue;
+                    }
+                    add_term(t, src, cf);
+                }
+                drop_zero_terms(t);
+            }
+            std::vector<std::pair<uint8_t*, Terms>> real;
+            collect = &real;
+            collect_eng = c.eng;
+            collect_B = c.B;
+            // virtual writes first: a new expression may read a block this same op overwrites, and the
+            // real writes below then write it out (into this op) like any other expression reading it.
+            // A virtual write leaves d's memory as it is, so expressions reading the real d stay valid.
+            for (int p = 0; p < m; p++) {
+                uint8_t* d = c.blocks[op.dst_ids[p]];
+                if (!scratch.holds(d, c.B)) continue;
+                for (auto& x : rows[p].second) users[x.first].push_back(d);
+                ex[d] = Expr{c.eng, c.st, c.B, std::move(rows[p].second)};
+            }
+            for (int p = 0; p < m; p++) {
+                uint8_t* d = c.blocks[op.dst_ids[p]];
+                if (scratch.holds(d, c.B)) continue;
+                before_write(d);
+                real.emplace_back(d, std::move(rows[p].second));
+            }
+            collect = nullptr;
+            if (!real.empty()) out.push_back(make_call(c.eng, c.st, c.B, real));
+        }
+    }
+    if (!scope_end && !ex.empty()) {  // a mid-scope flush leaves memory as the sequential calls would
+        std::vector<uint8_t*> left;
+        for (auto& kv : ex) left.push_back(kv.first);
+        std::sort(left.begin(), left.end());
+        write_out(left);
+    }
+    if (materialised) *materialised = nmat;
+    return out;
+}
+
+namespace {
+
+// Plan classes of a flush: calls with equal plans (by content), block size, stream and device share a
+// class.  Recording shares the plan pointer between consecutive equal calls, so most lookups hit the
+// pointer cache; composed calls are interned by content.
+class PlanClasses {
+public:
+    int of(const DeferredCall& c) {
+        auto pk = by_ptr_.find(c.ops.get());
+        int plan;
+        if (pk != by_ptr_.end()) {
+            plan = pk->second;
+        } else {
+            size_t h = 1469598103934665603ull;
+            auto mix = [&](const void* p, size_t n) {
+                const uint8_t* b = (const uint8_t*)p;
+                for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+            };
+            for (const LinearOp& op : *c.ops) {
+                mix(op.src_ids.data(), op.src_ids.size() * 4);
+                mix(op.dst_ids.data(), op.dst_ids.size() * 4);
+                mix(op.coef.data(), op.coef.size());
+                mix("|", 1);
+            }
+            plan = -1;
+            for (int id : by_hash_[h])
+                if (same_ops(*plans_[id], *c.ops)) plan = id;
+            if (plan < 0) {
+                plan = (int)plans_.size();
+                plans_.push_back(c.ops);
+                by_hash_[h].push_back(plan);
+            }
+            by_ptr_[c.ops.get()] = plan;
+        }
+        const auto key = std::make_tuple(plan, c.eng, c.st, c.B);
+        auto it = cls_.find(key);
+        if (it != cls_.end()) return it->second;
+        const int id = (int)cls_.size();
+        cls_.emplace(key, id);
+        return id;
+    }
+
+private:
+    std::unordered_map<const void*, int> by_ptr_;
+    std::unordered_map<size_t, std::vector<int>> by_hash_;
+    std::vector<std::shared_ptr<const std::vector<LinearOp>>> plans_;
+    std::map<std::tuple<int, Engine*, hipStream_t, long long>, int> cls_;
+};
+
+}  // namespace
 
 int batch_flush() {
     DeferScope& d = t_defer;
     if (d.q.empty()) return ECG_OK;
     std::vector<DeferredCall> q;
     q.swap(d.q);
-    // runs [i, j): same engine / stream / B / plan, and no block written by one call and touched by another
-    auto same_run = [&](size_t i, size_t j) {
-        return q[j].eng == q[i].eng && q[j].st == q[i].st && q[j].B == q[i].B &&
-               (q[j].ops == q[i].ops || same_ops(*q[j].ops, *q[i].ops));
-    };
+    FlushStats st;
+    st.recorded = (long long)q.size();
+    if (!d.scratch.empty()) q = compose_scratch(std::move(q), d.scratch, /*scope_end=*/!d.active, &st.materialised);
+    st.composed = (long long)q.size();
+    PlanClasses classes;
+    std::vector<int> cls(q.size());
+    for (size_t c = 0; c < q.size(); c++) cls[c] = classes.of(q[c]);
     auto reads = [&](size_t c, auto&& f) {
         for (const LinearOp& op : *q[c].ops)
             for (int id : op.src_ids) f(q[c].blocks[id]);
@@ -387,16 +690,18 @@ int batch_flush() {
         for (const LinearOp& op : *q[c].ops)
             for (int id : op.dst_ids) f(q[c].blocks[id]);
     };
-    const std::vector<size_t> ends = form_runs(q.size(), same_run, reads, writes);
+    const std::vector<std::vector<size_t>> groups =
+        schedule_groups(q.size(), [&](size_t c) { return cls[c]; }, reads, writes);
+    st.groups = (long long)groups.size();
     int caller_dev = -1, cur_dev = -1;
     (void)hipGetDevice(&caller_dev);
     cur_dev = caller_dev;
     int rc = ECG_OK;
-    size_t i = 0;
-    for (size_t r = 0; r < ends.size() && rc == ECG_OK; r++) {
-        const size_t j = ends[r];
-        Engine* eng = q[i].eng;
-        if (eng->device() != cur_dev) {  // a run launches on the device its calls were recorded on
+    for (size_t g = 0; g < groups.size() && rc == ECG_OK; g++) {
+        const std::vector<size_t>& G = groups[g];
+        const DeferredCall& c0 = q[G[0]];
+        Engine* eng = c0.eng;
+        if (eng->device() != cur_dev) {  // a group launches on the device its calls were recorded on
             if (hipSetDevice(eng->device()) != hipSuccess) {
                 set_last_error("batch flush: hipSetDevice failed");
                 rc = ECG_EHIP;
@@ -404,26 +709,32 @@ int batch_flush() {
             }
             cur_dev = eng->device();
         }
-        if (j - i == 1) {
-            rc = eng->launch_direct(*q[i].ops, q[i].blocks.data(), q[i].B, q[i].st);
-        } else {
-            std::vector<const uint8_t* const*> calls;
-            calls.reserve(j - i);
-            for (size_t c = i; c < j; c++) calls.push_back(q[c].blocks.data());
-            for (const LinearOp& op : *q[i].ops) {
-                if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
-                    for (size_t c = i; c < j && rc == ECG_OK; c++) rc = eng->launch_direct({op}, q[c].blocks.data(), q[c].B, q[c].st);
-                } else {
-                    bool done = false;
-                    rc = eng->run_calls_strided(op, calls, q[i].B, q[i].st, &done);
-                    if (rc == ECG_OK && !done) rc = eng->run_ptr_batch(op, calls, q[i].B, q[i].st);
-                }
-                if (rc != ECG_OK) break;
-            }
+        if (G.size() == 1) {
+            rc = eng->launch_direct(*c0.ops, c0.blocks.data(), c0.B, c0.st);
+            st.launches += (long long)c0.ops->size();
+            continue;
         }
-        i = j;
+        std::vector<const uint8_t* const*> calls;
+        calls.reserve(G.size());
+        for (size_t c : G) calls.push_back(q[c].blocks.data());
+        for (const LinearOp& op : *c0.ops) {
+            if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
+                for (size_t c : G) {
+                    rc = eng->launch_direct({op}, q[c].blocks.data(), q[c].B, q[c].st);
+                    st.launches++;
+                    if (rc != ECG_OK) break;
+                }
+            } else {
+                bool done = false;
+                rc = eng->run_calls_strided(op, calls, c0.B, c0.st, &done);
+                if (rc == ECG_OK && !done) rc = eng->run_ptr_batch(op, calls, c0.B, c0.st);
+                st.launches++;
+            }
+            if (rc != ECG_OK) break;
+        }
     }
     if (cur_dev != caller_dev && caller_dev >= 0) (void)hipSetDevice(caller_dev);
+    d.stats = st;
     return rc;
 }
 
@@ -431,9 +742,10 @@ int batch_flush_pending() { return t_defer.q.empty() ? ECG_OK : batch_flush(); }
 
 int batch_end() {
     if (!t_defer.active) return ECG_EINVAL;
+    t_defer.active = false;  // the flush below is the scope's end: unconsumed scratch is not written
     const int rc = batch_flush();
-    t_defer.active = false;
     t_defer.q.clear();
+    t_defer.scratch.clear();
     return rc;
 }
 

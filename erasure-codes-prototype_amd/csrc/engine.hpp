@@ -94,103 +94,149 @@ private:
 
 // Deferred-batch scope of the calling thread (ecg_batch_begin / ecg_batch_end).  Inside a scope,
 // device-tier calls (run_device: ecg_dev_matrix_*, ErasureCode objects on HBM buffers) are recorded
-// instead of launched; batch_flush() launches each run of consecutive calls with the same plan and
-// block size on the same stream as ONE launch per op -- strided when the run's blocks form one strided
-// batch, a pointer-table launch otherwise -- splitting a run where a call touches a block an earlier
-// call of the run writes (or writes one it reads).  Host-tier and batched calls flush first, so call
-// order is kept.
-// A flush launches each run on its engine's device (the calling thread's device is restored after).  If a
-// launch fails, the flush stops there and returns the error; the calls of that run and of every later
-// run are dropped (not retried by a later flush).
+// instead of launched.  batch_flush() then
+//   1. composes away scratch blocks (batch_scratch): a block written and later read inside the scope
+//      whose memory the caller declared scratch is never written -- its readers take the linear map
+//      that produced it instead (the helper partial + main partial + perform_addition sequence of a
+//      partial-decoding repair becomes one region product per repair, compose_scratch below);
+//   2. groups the calls (schedule_groups below): calls with the same plan, block size, stream and
+//      device join one group unless a data dependence orders them apart, and each group goes out as
+//      ONE launch per op -- strided when its blocks form one strided batch, a pointer-table launch
+//      otherwise.  Groups launch in an order that respects every read/write dependence of the recorded
+//      sequence, so the result is the sequential result.
+// Host-tier and batched calls flush first, so call order is kept.  A flush launches each group on its
+// engine's device (the calling thread's device is restored after).  If a launch fails, the flush stops
+// there and returns the error; the calls of that group and of every later group are dropped (not
+// retried by a later flush).
 int batch_begin();
 int batch_flush();
 int batch_end();
 bool batch_active();
+// Declare [p, p + bytes) scratch for the rest of the current scope (ECG_EINVAL outside a scope).
+int batch_scratch(const void* p, size_t bytes);
 // Flush this thread's recorded calls, if any (entry points that launch directly call it first, so a
 // recorded call never runs after a later direct launch).
 int batch_flush_pending();
+// What the last flush of this thread did: calls recorded, calls after scratch composition, launches
+// (groups x ops; byte-path tails not counted), scratch expressions materialised (written for real).
+struct FlushStats {
+    long long recorded = 0, composed = 0, groups = 0, launches = 0, materialised = 0;
+};
+FlushStats last_flush_stats();
 
-// Open-addressing set of block addresses for the flush's hazard check: a run of S recorded calls puts
-// S * (k + m) addresses through it, and node-based hashing made that check most of a flush.  Addresses
-// are never null (validated at record time), so 0 marks an empty slot.
-class PtrSet {
+// One recorded device-tier call: its plan (shared by calls with an equal plan) over its block space.
+struct DeferredCall {
+    Engine* eng;
+    hipStream_t st;
+    long long B;
+    std::shared_ptr<const std::vector<LinearOp>> ops;
+    std::vector<uint8_t*> blocks;  // device pointers
+};
+
+// Scratch ranges of a scope (merged, disjoint).  A block [p, p + B) is scratch if one range holds it.
+class ScratchRanges {
 public:
-    void clear() {  // O(table): shrink a table a large run left behind before many small runs reuse it
-        if (slots_.size() > 4096 && count_ * 8 < slots_.size()) {
-            slots_.assign(1024, 0);
-            mask_ = 1023;
-        } else if (count_) {
-            std::fill(slots_.begin(), slots_.end(), (uintptr_t)0);
-        }
-        count_ = 0;
-    }
-    bool contains(const void* ptr) const {
-        if (slots_.empty()) return false;
-        const uintptr_t p = (uintptr_t)ptr;
-        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
-            if (slots_[i] == p) return true;
-            if (slots_[i] == 0) return false;
-        }
-    }
-    void insert(const void* ptr) {
+    void add(uintptr_t lo, uintptr_t hi);
+    bool holds(const void* p, long long B) const;
+    bool empty() const { return r_.empty(); }
+    void clear() { r_.clear(); }
+
+private:
+    std::vector<std::pair<uintptr_t, uintptr_t>> r_;  // sorted by start, disjoint, [lo, hi)
+};
+
+// Scratch composition (pure host logic, no HIP; fuzzed in tests/sanitize/host_fuzz.cpp against a
+// sequential interpreter).  Walks the recorded calls in order, keeping for every scratch block written
+// so far the linear combination of real blocks it holds (an "expression").  A call reading a scratch
+// block with an expression reads that combination's blocks instead (coefficients multiplied out over
+// GF(2^8)); a call writing a scratch block only records the expression.  An expression is written for
+// real ("materialised") before any block it reads is overwritten, when a reader runs on another
+// stream / device / block size, and -- unless `scope_end` -- for every expression left at the end
+// (a mid-scope flush must leave memory as the sequential calls would).  At scope end unconsumed
+// scratch contents are undefined: that is the contract of batch_scratch.  Blocks are compared by
+// address, as in the hazard check (blocks of one scope are identical or disjoint).  Calls that touch
+// neither scratch nor an expression pass through unchanged (their plan pointer kept).
+std::vector<DeferredCall> compose_scratch(std::vector<DeferredCall>&& q, const ScratchRanges& scratch,
+                                          bool scope_end, long long* materialised);
+
+// Open-addressing map block address -> the latest group (index + 1) that read / wrote it, for the
+// flush's scheduler.  0 = never touched.
+class PtrGroups {
+public:
+    struct Slot {
+        uintptr_t p;
+        int rd, wr;
+    };
+    Slot& at(const void* ptr) {
         if ((count_ + 1) * 2 > slots_.size()) grow();
         const uintptr_t p = (uintptr_t)ptr;
         for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
-            if (slots_[i] == p) return;
-            if (slots_[i] == 0) {
-                slots_[i] = p;
+            if (slots_[i].p == p) return slots_[i];
+            if (slots_[i].p == 0) {
+                slots_[i] = Slot{p, 0, 0};
                 count_++;
-                return;
+                return slots_[i];
             }
         }
     }
-    size_t size() const { return count_; }
+    int last_write(const void* ptr) const { const Slot* s = find(ptr); return s ? s->wr : 0; }
+    int last_touch(const void* ptr) const { const Slot* s = find(ptr); return s ? std::max(s->rd, s->wr) : 0; }
 
 private:
+    const Slot* find(const void* ptr) const {
+        if (slots_.empty()) return nullptr;
+        const uintptr_t p = (uintptr_t)ptr;
+        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
+            if (slots_[i].p == p) return &slots_[i];
+            if (slots_[i].p == 0) return nullptr;
+        }
+    }
     static size_t hash(uintptr_t p) { return (size_t)(((unsigned long long)p >> 4) * 0x9E3779B97F4A7C15ull >> 17); }
     void grow() {
-        std::vector<uintptr_t> old;
+        std::vector<Slot> old;
         old.swap(slots_);
-        slots_.assign(old.empty() ? 1024 : old.size() * 2, 0);
+        slots_.assign(old.empty() ? 1024 : old.size() * 2, Slot{0, 0, 0});
         mask_ = slots_.size() - 1;
         count_ = 0;
-        for (uintptr_t p : old)
-            if (p) insert((const void*)p);
+        for (const Slot& s : old)
+            if (s.p) at((const void*)s.p) = s;
     }
-    std::vector<uintptr_t> slots_;
+    std::vector<Slot> slots_;
     size_t mask_ = 0, count_ = 0;
 };
 
-// Run formation of the flush (pure host logic, no HIP; fuzzed against a quadratic check in
-// tests/sanitize/host_fuzz.cpp).  Splits calls [0, n) into maximal runs [i, j): every call of a run has
-// same_run(i, c) true, and no call reads or writes a block an earlier call of its run writes, or writes a
-// block an earlier call of its run reads.  reads(c, f) / writes(c, f) call f(address) for each block call
-// c reads / writes.  Returns the run ends (the last one is n).
-template <class SameRun, class Reads, class Writes>
-std::vector<size_t> form_runs(size_t n, SameRun same_run, Reads reads, Writes writes) {
-    std::vector<size_t> ends;
-    PtrSet wr, rd;
-    size_t i = 0;
-    while (i < n) {
-        wr.clear();
-        rd.clear();
-        auto add = [&](size_t c) {
-            reads(c, [&](const void* p) { rd.insert(p); });
-            writes(c, [&](const void* p) { wr.insert(p); });
-        };
-        add(i);
-        size_t j = i + 1;
-        for (; j < n && same_run(i, j); j++) {
-            bool clash = false;
-            reads(j, [&](const void* p) { clash = clash || wr.contains(p); });
-            writes(j, [&](const void* p) { clash = clash || wr.contains(p) || rd.contains(p); });
-            if (clash) break;
-            add(j);
+// Grouping of the flush (pure host logic, no HIP; fuzzed against a quadratic legality check in
+// tests/sanitize/host_fuzz.cpp).  Calls [0, n) in program order; key(c) >= 0 names the call's plan
+// class (same plan, block size, stream, device).  Each call joins the LATEST group of its key if that
+// group comes after every group holding an earlier call it depends on (one that writes a block it reads
+// or writes, or reads a block it writes); otherwise it opens a new group at the end.  Launching the
+// groups in index order, each group's calls in one launch, therefore respects every dependence of the
+// program order (two dependent calls always sit in groups i < j), and independent calls of one plan --
+// the reference's per-stripe loop, even with several plans interleaved per stripe -- share a launch.
+// reads(c, f) / writes(c, f) call f(address) per block call c reads / writes.  Returns the groups,
+// each listing its calls in program order.
+template <class Key, class Reads, class Writes>
+std::vector<std::vector<size_t>> schedule_groups(size_t n, Key key, Reads reads, Writes writes) {
+    std::vector<std::vector<size_t>> groups;
+    std::vector<int> last_of_key;  // key -> latest group index + 1
+    PtrGroups seen;
+    for (size_t c = 0; c < n; c++) {
+        int lo = 0;  // the call must go into a group with index + 1 > lo
+        reads(c, [&](const void* p) { lo = std::max(lo, seen.last_write(p)); });
+        writes(c, [&](const void* p) { lo = std::max(lo, seen.last_touch(p)); });
+        const int kc = key(c);
+        if ((size_t)kc >= last_of_key.size()) last_of_key.resize((size_t)kc + 1, 0);
+        int g1 = last_of_key[kc];
+        if (g1 == 0 || g1 <= lo) {
+            groups.emplace_back();
+            g1 = (int)groups.size();
+            last_of_key[kc] = g1;
         }
-        ends.push_back(j);
-        i = j;
+        groups[(size_t)g1 - 1].push_back(c);
+        reads(c, [&](const void* p) { PtrGroups::Slot& s = seen.at(p); s.rd = std::max(s.rd, g1); });
+        writes(c, [&](const void* p) { PtrGroups::Slot& s = seen.at(p); s.wr = std::max(s.wr, g1); });
     }
-    return ends;
+    return groups;
 }
 
 // Last HIP error seen by this thread (for diagnostics through the C ABI).

@@ -63,7 +63,7 @@ EXPORTS = [
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
     "ecg_jerasure_invert_matrix", "ecg_jerasure_matrix_multiply", "ecg_galois_region_xor",
     "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode", "ecg_jerasure_matrix_dotprod",
-    "ecg_batch_begin", "ecg_batch_flush", "ecg_batch_end",
+    "ecg_batch_begin", "ecg_batch_flush", "ecg_batch_end", "ecg_batch_scratch", "ecg_batch_last_stats",
     "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
     "ecg_encode_batch",
     "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_make_decode_matrix", "ecg_region_xor_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
@@ -151,6 +151,8 @@ def lib():
         "ecg_batch_begin": ([], I),
         "ecg_batch_flush": ([], I),
         "ecg_batch_end": ([], I),
+        "ecg_batch_scratch": ([P, ctypes.c_size_t], I),
+        "ecg_batch_last_stats": ([ctypes.POINTER(LL)] * 4, I),
         "ecg_device_count": ([], I),
         "ecg_set_device": ([I], I),
         "ecg_free": ([P], None),
@@ -326,7 +328,9 @@ def jerasure_matrix_decode(k, m, matrix, row_k_ones, erasures, data, coding, siz
 
 class batch:
     """Deferred-batch scope (ecg_batch_begin / ecg_batch_end): per-stripe device-tier calls made by this
-    thread inside the `with` block are recorded and launched as batched pointer-table launches on exit."""
+    thread inside the `with` block are recorded and launched on exit, one launch per plan and op where no
+    data dependence orders the calls apart.  `scratch(t)` declares a device tensor (or (ptr, nbytes))
+    scratch: partial results written there and read later in the scope are composed away."""
 
     def __enter__(self):
         _check(lib().ecg_batch_begin(), "batch_begin")
@@ -335,11 +339,30 @@ class batch:
     def flush(self):
         _check(lib().ecg_batch_flush(), "batch_flush")
 
+    def scratch(self, t, nbytes=None):
+        batch_scratch(t, nbytes)
+
     def __exit__(self, exc_type, exc, tb):
         rc = lib().ecg_batch_end()
         if exc_type is None:
             _check(rc, "batch_end")
         return False
+
+
+def batch_scratch(t, nbytes=None):
+    """ecg_batch_scratch: a torch tensor (its whole storage span) or a device address + nbytes."""
+    if nbytes is None:
+        ptr, nbytes = t.data_ptr(), t.numel() * t.element_size()
+    else:
+        ptr = t if isinstance(t, int) else t.data_ptr()
+    _check(lib().ecg_batch_scratch(ctypes.c_void_p(ptr), nbytes), "batch_scratch")
+
+
+def batch_last_stats():
+    """What this thread's last flush did: {recorded, composed, launches, materialised}."""
+    v = [ctypes.c_longlong(0) for _ in range(4)]
+    _check(lib().ecg_batch_last_stats(*[ctypes.byref(x) for x in v]), "batch_last_stats")
+    return dict(zip(("recorded", "composed", "launches", "materialised"), (x.value for x in v)))
 
 
 def dev_matrix_encode(k, m, matrix, data, coding, B, stream=None):

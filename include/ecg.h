@@ -114,20 +114,37 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
  * (proxy.cpp:312-349); on HBM-resident blocks each such call is a separate small launch, bound by
  * launch cost (~8 us per RS(10,4) call).  Between ecg_batch_begin() and ecg_batch_end(), device-tier
  * calls of this thread (ecg_dev_matrix_* and ErasureCode handles in ECG_MEM_DEVICE mode) are only
- * validated and recorded; ecg_batch_end() (or ecg_batch_flush()) launches every run of consecutive
- * calls with the same plan, block size and stream as one launch per op, asynchronously on that
- * stream: a strided launch when the run's blocks are one strided batch (block b of the c-th call at
- * base + c * stripe_stride + b * block_stride, checked for every pointer), a pointer-table launch
- * otherwise.  Outputs are defined once the flush's work completes on the stream.  A run is split
- * where a call reads or writes a block an earlier call of the run writes, or writes one it reads
- * (blocks compared by address: partially overlapping blocks are not allowed).  Host-tier and batched
- * calls made inside the scope (ecg_region_xor_batch and ecg_fill_random included) flush first.  A run
- * launches on the device its calls were recorded on, whatever the thread's device at flush time.  If a
- * launch fails, the flush returns its error and the calls of that run and of all later runs are
- * discarded (the scope stays open, empty).  Scopes do not nest (ECG_EINVAL). */
+ * validated and recorded; ecg_batch_end() (or ecg_batch_flush()) launches them asynchronously on
+ * their streams.  Recorded calls with the same plan, block size, stream and device are grouped into
+ * ONE launch per op unless a data dependence orders them apart (a call reads or writes a block an
+ * earlier call writes, or writes one an earlier call reads), so a per-stripe loop that interleaves
+ * several plans -- a repair's helper partial, main partial and perform_addition per stripe -- still
+ * goes out as one launch per plan.  Groups launch in an order that keeps every such dependence: the
+ * outputs are the outputs of the calls run one by one, defined once the flush's work completes on the
+ * stream.  A group is a strided launch when its blocks are one strided batch (block b of the c-th call
+ * at base + c * stripe_stride + b * block_stride, checked for every pointer), a pointer-table launch
+ * otherwise.  Blocks are compared by address: blocks of one scope are identical or disjoint.
+ * Host-tier and batched calls made inside the scope (ecg_region_xor_batch and ecg_fill_random
+ * included) flush first.  A group launches on the device its calls were recorded on, whatever the
+ * thread's device at flush time.  If a launch fails, the flush returns its error and the calls of that
+ * group and of all later groups are discarded (the scope stays open, empty).  Scopes do not nest
+ * (ECG_EINVAL). */
 int ecg_batch_begin(void);
 int ecg_batch_flush(void);
 int ecg_batch_end(void);
+/* Declare the device range [ptr, ptr + bytes) SCRATCH for the rest of the calling thread's scope
+ * (ECG_EINVAL outside one).  A recorded call that writes a block inside scratch memory does not write
+ * it: the flush keeps the linear combination the block would hold, and later recorded calls that read
+ * the block read that combination's blocks instead.  So a partial result that only feeds a later call
+ * of the scope -- a helper or main proxy's partial decode (erasure_code.cpp:113-150) consumed by
+ * perform_addition (erasure_code.cpp:70-94) on the same GPU, handle_repair.cpp:249,371-376 -- costs no
+ * HBM write and re-read.  The combination is written for real when it must be: before a block it reads
+ * is overwritten, when it is read on another stream, device or block size, and at a mid-scope flush.
+ * After ecg_batch_end() the contents of scratch memory are undefined. */
+int ecg_batch_scratch(const void* ptr, size_t bytes);
+/* What this thread's last flush did: calls recorded, calls after scratch composition, launches (groups
+ * x ops), scratch combinations written for real.  Any pointer may be NULL. */
+int ecg_batch_last_stats(long long* recorded, long long* composed, long long* launches, long long* materialised);
 /* Generic region product: out[dst_ids[p]] = XOR_j coef[p*k_in+j] * in[src_ids[j]] for S stripes,
  * in block b of stripe s at in_base + s*in_sstride + b*in_bstride (likewise out). */
 int ecg_matrix_apply_batch(int k_in, int m_out, const int* coef, const int* src_ids, const int* dst_ids,

@@ -3,6 +3,7 @@
 // hooks), partitions, repair plans, index helpers -- over randomly drawn parameters, with the host
 // translation units compiled under -fsanitize=address,undefined.  No GPU call is made.
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -10,7 +11,8 @@
 #include <vector>
 
 #include "ecg.h"
-#include "engine.hpp"  // ecg::form_runs, ecg::PtrSet (pure host logic of the batch-scope flush)
+#include "engine.hpp"  // ecg::schedule_groups, ecg::compose_scratch (pure host logic of the batch-scope flush)
+#include "gf256.hpp"
 
 static std::mt19937_64 rng(12345);
 static int rnd(int lo, int hi) { return std::uniform_int_distribution<int>(lo, hi)(rng); }
@@ -179,73 +181,252 @@ static void decode_plans() {
     }
 }
 
-// Run formation of the batch-scope flush (ecg::form_runs) against a quadratic restatement of its rule,
-// over many runs per flush so PtrSet's clear / shrink / grow paths all execute under the sanitizers.
-static void run_formation() {
+// Grouping of the batch-scope flush (ecg::schedule_groups) against a quadratic legality check: every call
+// lands in exactly one group of its own key, dependent calls (write-after-read, read-after-write,
+// write-after-write on one address) sit in strictly ordered groups, and the group count equals a
+// quadratic restatement of the join rule.  Many groups per flush, so PtrGroups grows under the sanitizers.
+static void grouping() {
     struct Call {
-        int plan;
+        int key;
         std::vector<const void*> rd, wr;
     };
-    long long runs_seen = 0;
+    long long groups_seen = 0;
     for (int trial = 0; trial < 400; trial++) {
         const int n = rnd(1, trial % 10 == 0 ? 6000 : 300);
-        const int plans = rnd(1, 3);
-        // pool: addresses shared between calls (hazards) or mostly private (long runs, big tables)
+        const int keys = rnd(1, 16);
+        // pool: addresses shared between calls (dependences) or mostly private (large groups, big tables)
         const int pool = rnd(0, 2) ? n * 12 : rnd(2, 40);
         std::vector<Call> c(n);
         for (auto& x : c) {
-            x.plan = rnd(0, plans - 1) * (rnd(0, 9) == 0 ? 1 : 0);
+            x.key = rnd(0, keys - 1);
             const int nr = rnd(0, 5), nw = rnd(1, 3);
             for (int i = 0; i < nr; i++) x.rd.push_back((const void*)(uintptr_t)(0x1000 + 16 * rnd(0, pool)));
             for (int i = 0; i < nw; i++) x.wr.push_back((const void*)(uintptr_t)(0x1000 + 16 * rnd(0, pool)));
         }
-        auto same = [&](size_t i, size_t j) { return c[i].plan == c[j].plan; };
+        auto key = [&](size_t i) { return c[i].key; };
         auto reads = [&](size_t i, auto&& f) { for (auto p : c[i].rd) f(p); };
         auto writes = [&](size_t i, auto&& f) { for (auto p : c[i].wr) f(p); };
-        const std::vector<size_t> ends = ecg::form_runs((size_t)n, same, reads, writes);
-        // quadratic reference: extend while the plan matches and no earlier call of the run conflicts
-        size_t i = 0, r = 0;
-        while (i < (size_t)n) {
-            size_t j = i + 1;
-            for (; j < (size_t)n && c[j].plan == c[i].plan; j++) {
-                bool clash = false;
-                for (size_t e = i; e < j && !clash; e++) {
-                    for (auto p : c[j].rd) clash |= std::count(c[e].wr.begin(), c[e].wr.end(), p) > 0;
-                    for (auto p : c[j].wr)
-                        clash |= std::count(c[e].wr.begin(), c[e].wr.end(), p) + std::count(c[e].rd.begin(), c[e].rd.end(), p) > 0;
-                }
-                if (clash) break;
+        const auto groups = ecg::schedule_groups((size_t)n, key, reads, writes);
+        std::vector<int> g_of(n, -1);
+        for (size_t g = 0; g < groups.size(); g++) {
+            if (groups[g].empty()) abort();
+            for (size_t i = 0; i < groups[g].size(); i++) {
+                const size_t x = groups[g][i];
+                if (g_of[x] != -1 || c[x].key != c[groups[g][0]].key) abort();
+                if (i && groups[g][i - 1] >= x) abort();  // program order inside a group
+                g_of[x] = (int)g;
             }
-            if (r >= ends.size() || ends[r] != j) {
-                fprintf(stderr, "form_runs mismatch: trial %d run %zu\n", trial, r);
+        }
+        auto dep = [&](size_t a, size_t b) {  // b (later) depends on a
+            for (auto p : c[b].rd) if (std::count(c[a].wr.begin(), c[a].wr.end(), p)) return true;
+            for (auto p : c[b].wr)
+                if (std::count(c[a].wr.begin(), c[a].wr.end(), p) || std::count(c[a].rd.begin(), c[a].rd.end(), p)) return true;
+            return false;
+        };
+        // quadratic restatement of the join rule, and the legality of the result
+        std::vector<int> ref(n), last(keys, -1);
+        int ng = 0;
+        for (int b = 0; b < n; b++) {
+            int lo = -1;
+            for (int a = 0; a < b; a++) {
+                if (g_of[a] == -1) abort();
+                if (dep((size_t)a, (size_t)b)) {
+                    if (g_of[a] >= g_of[b]) {
+                        fprintf(stderr, "schedule_groups: dependence %d -> %d not ordered (trial %d)\n", a, b, trial);
+                        abort();
+                    }
+                    lo = std::max(lo, ref[a]);
+                }
+            }
+            if (last[c[b].key] > lo) ref[b] = last[c[b].key];
+            else ref[b] = last[c[b].key] = ng++;
+            if (ref[b] != g_of[b]) {
+                fprintf(stderr, "schedule_groups: call %d in group %d, rule says %d (trial %d)\n", b, g_of[b], ref[b], trial);
                 abort();
             }
-            i = j;
-            r++;
         }
-        if (r != ends.size()) abort();
-        runs_seen += (long long)r;
+        if ((size_t)ng != groups.size()) abort();
+        groups_seen += ng;
     }
-    // PtrSet alone: grow past 1024 slots, shrink on clear, duplicates, membership after regrowth
-    ecg::PtrSet s;
-    for (int round = 0; round < 6; round++) {
-        const int cnt = round % 2 ? 20000 : 7;
-        for (int i = 1; i <= cnt; i++) s.insert((const void*)(uintptr_t)(i * 48));
-        for (int i = 1; i <= cnt; i++) s.insert((const void*)(uintptr_t)(i * 48));
-        if (s.size() != (size_t)cnt) abort();
-        for (int i = 1; i <= cnt; i++)
-            if (!s.contains((const void*)(uintptr_t)(i * 48))) abort();
-        if (s.contains((const void*)(uintptr_t)(cnt * 48 + 48))) abort();
-        s.clear();
-        if (s.size() != 0 || s.contains((const void*)(uintptr_t)48)) abort();
+    printf("grouping: %lld groups checked\n", groups_seen);
+}
+
+// Scratch composition (ecg::compose_scratch) + grouping against a sequential interpreter over real host
+// bytes: random multi-op calls over a pool of 8-byte blocks, some of them scratch, some calls on a second
+// "stream".  The composed calls, run in program order AND in the scheduler's group order, must leave every
+// non-scratch block as the recorded calls run one by one do (and every block, scratch included, for a
+// mid-scope flush, which writes leftover expressions out).  Engines and streams are never dereferenced.
+static void scratch_composition() {
+    constexpr int BS = 8;
+    auto run_op = [&](const ecg::LinearOp& op, uint8_t* const* blocks) {  // read all inputs, then write
+        std::vector<std::array<uint8_t, BS>> o(op.m_out());
+        for (int p = 0; p < op.m_out(); p++) {
+            o[p].fill(0);
+            for (int j = 0; j < op.k_in(); j++)
+                for (int x = 0; x < BS; x++)
+                    o[p][x] ^= (uint8_t)ecg::gf::mul(op.coef[(size_t)p * op.k_in() + j], blocks[op.src_ids[j]][x]);
+        }
+        for (int p = 0; p < op.m_out(); p++) memcpy(blocks[op.dst_ids[p]], o[p].data(), BS);
+    };
+    ecg::Engine* eng = (ecg::Engine*)(uintptr_t)0x10;
+    long long mats = 0, calls_in = 0, calls_out = 0;
+    for (int trial = 0; trial < 3000; trial++) {
+        const int P = rnd(2, 24), n = rnd(1, std::min(60, 2 + trial / 40));
+        std::vector<uint8_t> mem0((size_t)P * BS);
+        for (auto& b : mem0) b = (uint8_t)rnd(0, 255);
+        ecg::ScratchRanges scr;
+        std::vector<char> is_scr(P, 0);
+        for (int b = 0; b < P; b++)
+            if (rnd(0, 2) == 0) {
+                is_scr[b] = 1;
+                scr.add((uintptr_t)&mem0[(size_t)b * BS], (uintptr_t)&mem0[(size_t)b * BS] + BS);
+            }
+        std::vector<ecg::DeferredCall> q;
+        for (int i = 0; i < n; i++) {
+            const int nb = rnd(2, 6);
+            ecg::DeferredCall c{eng, (hipStream_t)(uintptr_t)(rnd(0, 7) == 0 ? 2 : 1), BS, nullptr, {}};
+            for (int b = 0; b < nb; b++) c.blocks.push_back(&mem0[(size_t)rnd(0, P - 1) * BS]);
+            auto ops = std::make_shared<std::vector<ecg::LinearOp>>();
+            const int nops = rnd(1, 2);
+            for (int o = 0; o < nops; o++) {
+                ecg::LinearOp op;
+                const int k = rnd(1, nb - 1), m = rnd(1, std::min(3, nb - k));
+                std::vector<int> ids(nb);
+                for (int b = 0; b < nb; b++) ids[b] = b;
+                std::shuffle(ids.begin(), ids.end(), rng);
+                op.src_ids.assign(ids.begin(), ids.begin() + k);
+                op.dst_ids.assign(ids.begin() + k, ids.begin() + k + m);
+                if (rnd(0, 4) == 0) op.dst_ids[0] = op.src_ids[0];  // in place (galois_region_xor shape)
+                for (int x = 0; x < k * m; x++) op.coef.push_back((uint8_t)(rnd(0, 3) == 0 ? 0 : rnd(0, 1) ? 1 : rnd(0, 255)));
+                ops->push_back(op);
+            }
+            c.ops = ops;
+            q.push_back(c);
+        }
+        const bool scope_end = rnd(0, 1);
+        // one trial: false (and a dump if `verbose`) when a composed order differs from the sequential one
+        auto verify = [&](const std::vector<ecg::DeferredCall>& q, bool verbose) {
+            std::vector<uint8_t> ref = mem0;
+            auto rebase = [&](uint8_t* p, std::vector<uint8_t>& m) { return m.data() + (p - mem0.data()); };
+            for (auto& c : q) {
+                std::vector<uint8_t*> bl;
+                for (auto p : c.blocks) bl.push_back(rebase(p, ref));
+                for (auto& op : *c.ops) run_op(op, bl.data());
+            }
+            long long nm = 0;
+            std::vector<ecg::DeferredCall> q2 = ecg::compose_scratch(std::vector<ecg::DeferredCall>(q), scr, scope_end, &nm);
+            if (!verbose) {
+                mats += nm;
+                calls_in += (long long)q.size();
+                calls_out += (long long)q2.size();
+            }
+            auto dump = [&](const std::vector<ecg::DeferredCall>& v, const char* name) {
+                fprintf(stderr, "%s:\n", name);
+                for (auto& c : v) {
+                    fprintf(stderr, " st%d", (int)(uintptr_t)c.st);
+                    for (auto& op : *c.ops) {
+                        fprintf(stderr, " [");
+                        for (int p = 0; p < op.m_out(); p++) {
+                            const long d = (long)((c.blocks[op.dst_ids[p]] - mem0.data()) / BS);
+                            fprintf(stderr, " b%ld%s=", d, is_scr[d] ? "s" : "");
+                            for (int j = 0; j < op.k_in(); j++)
+                                fprintf(stderr, "%d*b%d+", op.coef[(size_t)p * op.k_in() + j],
+                                        (int)((c.blocks[op.src_ids[j]] - mem0.data()) / BS));
+                        }
+                        fprintf(stderr, " ]");
+                    }
+                    fprintf(stderr, "\n");
+                }
+            };
+            auto same = [&](std::vector<uint8_t>& got, const char* what) {
+                for (int b = 0; b < P; b++) {
+                    if (scope_end && is_scr[b]) continue;
+                    if (memcmp(&got[(size_t)b * BS], &ref[(size_t)b * BS], BS)) {
+                        if (verbose) {
+                            fprintf(stderr, "scratch composition (%s, scope_end %d): block %d differs, trial %d\n", what,
+                                    (int)scope_end, b, trial);
+                            dump(q, "recorded");
+                            dump(q2, "composed");
+                        }
+                        return false;
+                    }
+                }
+                return true;
+            };
+            std::vector<uint8_t> seq = mem0;
+            for (auto& c : q2) {
+                std::vector<uint8_t*> bl;
+                for (auto p : c.blocks) bl.push_back(rebase(p, seq));
+                for (auto& op : *c.ops) run_op(op, bl.data());
+            }
+            if (!same(seq, "program order")) return false;
+            // group order: key = plan content + stream
+            std::vector<int> key(q2.size());
+            std::vector<std::pair<const std::vector<ecg::LinearOp>*, hipStream_t>> seen;
+            for (size_t i = 0; i < q2.size(); i++) {
+                int id = -1;
+                for (size_t s = 0; s < seen.size(); s++) {
+                    const auto& a = *seen[s].first;
+                    const auto& b = *q2[i].ops;
+                    bool eq = a.size() == b.size() && seen[s].second == q2[i].st;
+                    for (size_t o = 0; eq && o < a.size(); o++)
+                        eq = a[o].src_ids == b[o].src_ids && a[o].dst_ids == b[o].dst_ids && a[o].coef == b[o].coef;
+                    if (eq) id = (int)s;
+                }
+                if (id < 0) {
+                    id = (int)seen.size();
+                    seen.emplace_back(q2[i].ops.get(), q2[i].st);
+                }
+                key[i] = id;
+            }
+            auto reads = [&](size_t c, auto&& f) { for (auto& op : *q2[c].ops) for (int id : op.src_ids) f(q2[c].blocks[id]); };
+            auto writes = [&](size_t c, auto&& f) { for (auto& op : *q2[c].ops) for (int id : op.dst_ids) f(q2[c].blocks[id]); };
+            const auto groups = ecg::schedule_groups(q2.size(), [&](size_t c) { return key[c]; }, reads, writes);
+            std::vector<uint8_t> grp = mem0;
+            for (auto& G : groups)
+                for (size_t o = 0; o < q2[G[0]].ops->size(); o++) {
+                    // one launch: every call of the group reads before any call writes (independent calls)
+                    std::vector<std::vector<uint8_t>> snap;
+                    for (size_t c : G) {
+                        std::vector<uint8_t> tmp = grp;
+                        std::vector<uint8_t*> bl;
+                        for (auto p : q2[c].blocks) bl.push_back(rebase(p, tmp));
+                        run_op((*q2[c].ops)[o], bl.data());
+                        snap.push_back(tmp);
+                    }
+                    for (size_t i = 0; i < G.size(); i++) {
+                        const ecg::LinearOp& op = (*q2[G[i]].ops)[o];
+                        for (int id : op.dst_ids) {
+                            const size_t off = (size_t)(q2[G[i]].blocks[id] - mem0.data());
+                            memcpy(&grp[off], &snap[i][off], BS);
+                        }
+                    }
+                }
+            return same(grp, "group order");
+        };
+        if (!verify(q, false)) {  // shrink to a minimal failing call list, then show it
+            for (bool shrunk = true; shrunk;) {
+                shrunk = false;
+                for (size_t i = 0; i < q.size() && !shrunk; i++) {
+                    std::vector<ecg::DeferredCall> r = q;
+                    r.erase(r.begin() + (long)i);
+                    if (!verify(r, false)) {
+                        q = r;
+                        shrunk = true;
+                    }
+                }
+            }
+            verify(q, true);
+            abort();
+        }
     }
-    printf("run formation: %lld runs checked\n", runs_seen);
+    printf("scratch composition: %lld calls in, %lld out, %lld expressions materialised\n", calls_in, calls_out, mats);
 }
 
 // Deferred-batch scope bookkeeping (record, hazard-split runs, strided-run detection) over fake device
 // addresses.  Only where no GPU exists: the flush then stops at its first launch with ECG_EHIP (a
-// program-table allocation), so only the first run is launched; the run boundaries of every flush are
-// covered by run_formation() above.  With a GPU the fake addresses would be launched.
+// program-table allocation), so only the first group is launched; the grouping of every flush is
+// covered by grouping() above.  With a GPU the fake addresses would be launched.
 static void batch_scope() {
     if (ecg_device_count() > 0) return;
     ecg_coding_parameters cp{};
@@ -271,10 +452,12 @@ static void batch_scope() {
 }
 
 int main() {
+    if (const char* e = getenv("ECG_FUZZ_SEED")) rng.seed(strtoull(e, nullptr, 10));
     matrices();
     facade();
     decode_plans();
-    run_formation();
+    grouping();
+    scratch_composition();
     batch_scope();
     printf("host fuzz done\n");
     return 0;

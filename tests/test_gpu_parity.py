@@ -1000,6 +1000,154 @@ def test_batch_scope_flush_on_recording_device(ecg, torch_cuda):
     assert torch.equal(a, ref)
 
 
+def _azure_repair_state(ecg, torch, S, B, seed):
+    """Azure-LRC(12,2,2) stripes [S][16][B] on the GPU, block e = s mod 14 of stripe s lost (local repairs:
+    data and local parities), with the helper / main split of handle_repair.cpp."""
+    from bench import azure_local_split
+    k, l, g = 12, 2, 2
+    cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
+    ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)
+    st = torch.empty((S, k + g + l, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, seed)
+    ecg.encode_batch(k, g + l, ec.make_encoding_matrix(), st[:, :k], st[:, k:])
+    local = [e for e in range(16) if e not in (12, 13)]
+    plan = [(local[s % len(local)],) + azure_local_split(local[s % len(local)]) for s in range(S)]
+    return ec, st, plan
+
+
+def _repair_sequence(ec, st, plan, partials, out, B):
+    """The reference's partial-decoding repair of every stripe, call by call (handle_repair.cpp:249,
+    371-376): helper partial, main partial, perform_addition of the two."""
+    for s, (e, surv, sets) in enumerate(plan):
+        for i in range(2):
+            ec.encode_partial_blocks_for_decoding([st[s, b] for b in sets[i]], [partials[s, i]], B, sets[i], surv, [e])
+        ec.perform_addition([partials[s, 0], partials[s, 1]], [out[s]], B, 2, 1)
+
+
+def test_batch_scope_interleaved_plans_group(ecg, torch_cuda):
+    """Per-stripe repairs interleave three plans per stripe and a different erasure per stripe; the scope
+    still launches one launch per distinct plan (calls reordered where nothing orders them), and the
+    bytes are the sequential ones."""
+    torch = torch_cuda
+    S, B = 56, 64 * 1024
+    ec, st, plan = _azure_repair_state(ecg, torch, S, B, 0x5C0)
+    partials = torch.zeros((S, 2, B), dtype=torch.uint8, device="cuda")
+    out = torch.zeros((S, B), dtype=torch.uint8, device="cuda")
+    with ecg.batch():
+        _repair_sequence(ec, st, plan, partials, out, B)
+    torch.cuda.synchronize()
+    stats = ecg.batch_last_stats()
+    idx = torch.arange(S, device="cuda")
+    want = st[idx, torch.tensor([p[0] for p in plan], device="cuda")]
+    assert torch.equal(out, want)
+    assert stats["recorded"] == 3 * S and stats["composed"] == 3 * S
+    # one launch per distinct plan (partial plans are equal when their coefficient rows are: Azure's local
+    # rows are all ones, so every helper and main partial shares one plan), + the perform_addition plan
+    plans = {tuple(ec.partial_decoding_matrix(sets[i], surv, [e])) for e, surv, sets in plan for i in range(2)}
+    assert stats["launches"] == len(plans) + 1, (stats, plans)
+
+
+def test_batch_scope_scratch_composes_partials(ecg, oracle, torch_cuda):
+    """batch_scratch on the partial buffers: the helper partial + main partial + perform_addition of
+    every stripe compose into ONE region product per repair (7 block moves instead of 11), the partial
+    buffers are never written, and the repaired blocks equal the lost ones (and the oracle's repair)."""
+    torch = torch_cuda
+    S, B = 56, 64 * 1024 + 16  # + 16: byte-path tails too
+    ec, st, plan = _azure_repair_state(ecg, torch, S, B, 0x5C1)
+    partials = torch.full((S, 2, B), 0xA5, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((S, B), dtype=torch.uint8, device="cuda")
+    with ecg.batch() as scope:
+        scope.scratch(partials)
+        _repair_sequence(ec, st, plan, partials, out, B)
+    torch.cuda.synchronize()
+    stats = ecg.batch_last_stats()
+    idx = torch.arange(S, device="cuda")
+    want = st[idx, torch.tensor([p[0] for p in plan], device="cuda")]
+    assert torch.equal(out, want)
+    assert bool((partials == 0xA5).all()), "scratch partials were written"
+    composed = {tuple(ec.partial_decoding_matrix(surv, surv, [e])) for e, surv, _ in plan}
+    assert stats == {"recorded": 3 * S, "composed": S, "launches": len(composed), "materialised": 0}, stats
+    # the composed map of one stripe is the oracle's full local repair of that block
+    host = st[:2].cpu().numpy()
+    for s in range(2):
+        e, surv, _ = plan[s]
+        R = ec.partial_decoding_matrix(surv, surv, [e])
+        rebuilt = np.zeros(B, np.uint8)
+        oracle.jerasure_matrix_encode(len(surv), 1, list(R), [host[s, b] for b in surv], [rebuilt], B)
+        assert np.array_equal(rebuilt, out[s].cpu().numpy())
+
+
+def test_batch_scope_scratch_mid_scope_flush_and_streams(ecg, torch_cuda):
+    """A scratch partial still pending at a mid-scope flush is written for real (memory as if the calls
+    ran one by one); one read on another stream is written for real before that read; one never read is
+    not written at scope end."""
+    torch = torch_cuda
+    S, B = 8, 4096
+    ec, st, plan = _azure_repair_state(ecg, torch, S, B, 0x5C2)
+    partials = torch.full((S, 2, B), 0x3C, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((S, B), dtype=torch.uint8, device="cuda")
+    ref_p = torch.zeros_like(partials)
+    ref_o = torch.zeros_like(out)
+    _repair_sequence(ec, st, plan, ref_p, ref_o, B)  # outside any scope: the sequential bytes
+    torch.cuda.synchronize()
+    with ecg.batch() as scope:
+        scope.scratch(partials)
+        for s, (e, surv, sets) in enumerate(plan):
+            for i in range(2):
+                ec.encode_partial_blocks_for_decoding([st[s, b] for b in sets[i]], [partials[s, i]], B, sets[i], surv, [e])
+        scope.flush()
+        torch.cuda.synchronize()
+        assert torch.equal(partials, ref_p), "mid-scope flush must write pending scratch"
+        assert ecg.batch_last_stats()["materialised"] == 2 * S
+    # another stream reads a scratch partial: written for real first, on the producer's stream
+    partials.fill_(0x3C)
+    side = torch.cuda.Stream()
+    with ecg.batch() as scope:
+        scope.scratch(partials)
+        for s, (e, surv, sets) in enumerate(plan):
+            for i in range(2):
+                ec.encode_partial_blocks_for_decoding([st[s, b] for b in sets[i]], [partials[s, i]], B, sets[i], surv, [e])
+        ec.perform_addition([partials[0, 0], partials[0, 1]], [out[0]], B, 2, 1, stream=side)
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], ref_o[0])
+    assert torch.equal(partials[0], ref_p[0])
+    assert bool((partials[1:] == 0x3C).all()), "unconsumed scratch must not be written at scope end"
+
+
+def test_batch_scope_random_sequences(ecg, torch_cuda):
+    """Random per-call region products (dev_matrix_encode over blocks drawn from a small pool, so calls
+    depend on each other, some blocks scratch) inside a scope, against the same calls run one by one
+    outside any scope; non-scratch blocks must match exactly."""
+    torch = torch_cuda
+    rng = random.Random(0xF00D)
+    B, P = 256, 12
+    for trial in range(30):
+        pool0 = torch.randint(0, 256, (P, B), dtype=torch.uint8, device="cuda")
+        scratch = [b for b in range(P) if rng.random() < 0.3]
+        calls = []
+        for _ in range(rng.randint(1, 40)):
+            k, m = rng.randint(1, 4), rng.randint(1, 3)
+            ids = rng.sample(range(P), k + m) if rng.random() < 0.8 else [rng.randrange(P) for _ in range(k + m)]
+            M = [rng.choice([0, 1, 1, rng.randrange(256)]) for _ in range(k * m)]
+            calls.append((k, m, M, ids))
+
+        def run(pool):
+            for k, m, M, ids in calls:
+                ecg.dev_matrix_encode(k, m, M, [pool[i] for i in ids[:k]], [pool[i] for i in ids[k:]], B)
+
+        seq = pool0.clone()
+        run(seq)
+        got = pool0.clone()
+        with ecg.batch() as scope:
+            for b in scratch:
+                scope.scratch(got[b])
+            run(got)
+        torch.cuda.synchronize()
+        keep = [b for b in range(P) if b not in scratch]
+        assert torch.equal(got[keep], seq[keep]), (trial, calls, scratch)
+
+
 # ------------------------------------------------------------------ randomized code parameters, every family
 
 def _random_configs(n, seed):
