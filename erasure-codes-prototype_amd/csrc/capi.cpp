@@ -57,6 +57,7 @@ int ecg_set_device(int device) { return hipSetDevice(device) == hipSuccess ? ECG
 void ecg_free(void* p) { free(p); }
 
 int ecg_program_cache_size(void) { return (int)Engine::instance().cache_size(); }
+int ecg_program_sets_retiring(void) { return (int)Engine::instance().retired_pending(); }
 int ecg_host_contexts(void) { return Engine::instance().host_contexts(); }
 
 int ecg_batch_begin(void) { return batch_begin(); }
@@ -116,8 +117,21 @@ int* ecg_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int 
     return to_malloc(matrix_multiply(m1, m2, r1, c1, r2, c2));
 }
 
+// The reference calls galois_region_xor itself only inside its Cauchy-LRC matrix builders, to add the
+// global rows' int coefficients into a local row (lrc.cpp:1511,2140: 4 * k bytes of host matrix), and
+// rebuilds those matrices on every call (lrc.cpp:27).  Regions up to kHostXorMax bytes are that matrix
+// work (host-side, keep on CPU) and are XORed in place here; a GPU round trip
+// (~15 us) per coefficient row would cost more than the whole encode of a small stripe.  Larger
+// regions -- block data -- run on the GPU like every other region product.
+constexpr int kHostXorMax = 4096;
+
 int ecg_galois_region_xor(char* src, char* dest, int nbytes) {
     if (nbytes < 0 || !src || !dest) return ECG_EINVAL;
+    if (nbytes <= kHostXorMax) {
+        if (const int rc = batch_flush_pending(); rc != ECG_OK) return rc;  // host-tier call order, as run_host
+        for (int i = 0; i < nbytes; i++) dest[i] ^= src[i];
+        return ECG_OK;
+    }
     LinearOp op;
     op.src_ids = {0, 1};
     op.dst_ids = {1};

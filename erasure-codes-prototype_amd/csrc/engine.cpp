@@ -101,14 +101,62 @@ private:
 const char* last_error_string() { return t_last_error.c_str(); }
 void set_last_error(const std::string& s) { t_last_error = s; }
 
-// A set is destroyed only after the cache dropped it AND every caller released it; kernels already
-// enqueued may still read its tables, so wait for the device before freeing (eviction is rare: at
-// most once per ECG_OPT_PROGRAM_CACHE / 2 new programs).
+// Freed without waiting: a set that was ever launched is destroyed only by sweep_retired(), after its
+// launches completed; any other (a lost insertion race, a failed build) was never launched.
 ProgramSet::~ProgramSet() {
-    if (d_tabs || d_src || d_dst) (void)hipDeviceSynchronize();
     if (d_tabs) (void)hipFree(d_tabs);
     if (d_src) (void)hipFree(d_src);
     if (d_dst) (void)hipFree(d_dst);
+}
+
+void Engine::retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted) {
+    std::lock_guard<std::mutex> lk(rmu_);
+    for (auto& ps : evicted) retired_.push_back(Retired{std::move(ps), {}, false});
+}
+
+void Engine::sweep_retired() {
+    std::vector<std::shared_ptr<ProgramSet>> dead;  // freed outside the lock
+    {
+        std::lock_guard<std::mutex> lk(rmu_);
+        bool sync_all = false;
+        for (Retired& r : retired_) {
+            if (r.armed || r.ps.use_count() != 1) continue;
+            // nobody holds the set any more, so every launch that reads it is already enqueued
+            std::lock_guard<std::mutex> sk(r.ps->smu);
+            if (r.ps->overflow) sync_all = true;
+            for (int i = 0; i < r.ps->nstreams && !sync_all; i++) {
+                hipEvent_t ev = nullptr;
+                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                    hipEventRecord(ev, r.ps->streams[i]) != hipSuccess) {
+                    if (ev) (void)hipEventDestroy(ev);
+                    sync_all = true;  // e.g. a caller's stream destroyed since: fall back to the device
+                    break;
+                }
+                r.evs.push_back(ev);
+            }
+            r.armed = true;
+        }
+        if (sync_all) (void)hipDeviceSynchronize();
+        for (size_t i = 0; i < retired_.size();) {
+            Retired& r = retired_[i];
+            bool done = r.armed;
+            for (size_t e = 0; done && e < r.evs.size(); e++) done = sync_all || hipEventQuery(r.evs[e]) == hipSuccess;
+            if (!done) {
+                i++;
+                continue;
+            }
+            for (hipEvent_t ev : r.evs) (void)hipEventDestroy(ev);
+            dead.push_back(std::move(r.ps));
+            retired_[i] = std::move(retired_.back());
+            retired_.pop_back();
+        }
+    }
+}
+
+size_t Engine::retired_pending() {
+    sweep_retired();
+    std::lock_guard<std::mutex> lk(rmu_);
+    return retired_.size();
 }
 
 Engine::Engine(int device) : device_(device) {}
@@ -206,7 +254,7 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
         return fail(e, "hipMemcpy(src)");
     if ((e = hipMemcpy(ps->d_dst, dst.data(), dst.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "hipMemcpy(dst)");
-    std::vector<std::shared_ptr<ProgramSet>> evicted;  // destroyed outside the lock
+    std::vector<std::shared_ptr<ProgramSet>> evicted;  // retired outside the lock
     {
         std::lock_guard<std::mutex> lk(mu_);
         auto it = cache_.find(key);
@@ -233,7 +281,8 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
         }
         cache_.emplace(std::move(key), CacheEntry{ps, ++tick_});
     }
-    evicted.clear();
+    if (!evicted.empty()) retire(std::move(evicted));
+    sweep_retired();
     return ps;
 }
 
@@ -267,6 +316,7 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     for (int s : op.src_ids) vec_ok &= aligned16(blocks[s]);
     for (int j = 0; j < op.k_in(); j++) a.isrc[j] = blocks[op.src_ids[j]];
     for (int p = 0; p < op.m_out(); p++) a.idst[p] = blocks[op.dst_ids[p]];
+    ps->used_on(st);
     ECG_HIP(launch_gf(a, GF_MODE_INLINE, vec_ok, st));
     return ECG_OK;
 }
@@ -1005,6 +1055,7 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
     a.binary = ps->binary ? 1 : 0;
     const bool vec_ok = aligned16(in_base) && aligned16(out_base) && (in_sstride % 16 == 0) &&
                         (in_bstride % 16 == 0) && (out_sstride % 16 == 0) && (out_bstride % 16 == 0);
+    ps->used_on(st);
     ECG_HIP(launch_gf(a, GF_MODE_STRIDED, vec_ok, st));
     return ECG_OK;
 }
@@ -1031,6 +1082,7 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
     a.MT = ps->MT;
     a.rtiles = ps->rtiles;
     a.binary = ps->binary ? 1 : 0;
+    ps->used_on(st);
     ECG_HIP(launch_gf(a, GF_MODE_PTRS, aligned, st));
     return ECG_OK;
 }
@@ -1077,6 +1129,7 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     std::shared_ptr<ProgramSet> ps = program_set({dev}, &status);
     if (!ps) return status;
     hipStream_t s_in = c.pstream[0], s_comp = c.pstream[1], s_out = c.pstream[2];
+    ps->used_on(s_comp);
     const uint8_t* hin = (const uint8_t*)h_in;
     uint8_t* hout = (uint8_t*)h_out;
     bool used[3] = {false, false, false};

@@ -40,7 +40,21 @@ struct ProgramSet {
     int* d_dst = nullptr;
     int nprog = 0, k = 0, m = 0, MT = 1, rtiles = 1;
     bool binary = false;
-    ~ProgramSet();
+    // streams the set's tables were launched on (for its retirement after eviction: a completion event
+    // per stream instead of a device-wide synchronize); more than kMaxStreams -> synchronize the device
+    static constexpr int kMaxStreams = 8;
+    std::mutex smu;
+    hipStream_t streams[kMaxStreams] = {};
+    int nstreams = 0;
+    bool overflow = false;
+    void used_on(hipStream_t s) {
+        std::lock_guard<std::mutex> lk(smu);
+        for (int i = 0; i < nstreams; i++)
+            if (streams[i] == s) return;
+        if (nstreams < kMaxStreams) streams[nstreams++] = s;
+        else overflow = true;
+    }
+    ~ProgramSet();  // frees at once: only reached when no launch can still read the tables
 };
 
 class Engine {
@@ -82,6 +96,12 @@ private:
     explicit Engine(int device);
     int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream);
 
+    // Evicted sets wait here until nothing can read their tables: first until no caller holds them (no
+    // further launch can be enqueued), then until a completion event recorded on every stream they were
+    // launched on has fired.  Swept on every cache miss; no device-wide synchronize on this path.
+    void retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted);
+    void sweep_retired();
+
     int device_;
     struct CacheEntry {
         std::shared_ptr<ProgramSet> ps;
@@ -90,6 +110,16 @@ private:
     std::mutex mu_;
     uint64_t tick_ = 0;
     std::unordered_map<std::string, CacheEntry> cache_;  // LRU-bounded by ECG_OPT_PROGRAM_CACHE
+    struct Retired {
+        std::shared_ptr<ProgramSet> ps;
+        std::vector<hipEvent_t> evs;
+        bool armed = false;
+    };
+    std::mutex rmu_;
+    std::vector<Retired> retired_;
+
+public:
+    size_t retired_pending();  // evicted sets not yet freed (tests)
 };
 
 // Deferred-batch scope of the calling thread (ecg_batch_begin / ecg_batch_end).  Inside a scope,

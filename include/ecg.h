@@ -42,6 +42,9 @@ int ecg_device_count(void);
 int ecg_set_device(int device);    /* selects the HIP device for the calling thread */
 void ecg_free(void* p);            /* frees matrices returned by this library (malloc'd, like Jerasure) */
 int ecg_program_cache_size(void);  /* programs cached for the current device (diagnostics) */
+/* Evicted program tables of the current device not yet freed: each waits for its launches to complete
+ * (a completion event per stream it ran on, never a device-wide synchronize).  Diagnostics. */
+int ecg_program_sets_retiring(void);
 /* Host-tier contexts (stream + device scratch + pinned staging) created so far for the current device
  * (diagnostics).  Contexts are pooled and leased per call, so this is bounded by the most host-tier calls
  * ever in flight at once, not by the number of threads that called (the reference's proxy starts a
@@ -77,7 +80,10 @@ int ecg_cauchy_n_ones(int n, int w);
 int ecg_jerasure_invert_matrix(int* mat, int* inv, int rows, int w);
 /* Replaces jerasure_matrix_multiply            (called erasure_code.cpp:131; lrc.cpp:969,1203,1558,2197) */
 int* ecg_jerasure_matrix_multiply(int* m1, int* m2, int r1, int c1, int r2, int c2, int w);
-/* Replaces galois_region_xor(src, dest, nbytes): dest ^= src (host buffers, computed on the GPU) */
+/* Replaces galois_region_xor(src, dest, nbytes): dest ^= src (host buffers).  Regions above 4096 bytes
+ * (block data) are computed on the GPU.  Up to 4096 bytes -- what the reference's own calls pass: the
+ * int coefficient rows of its Cauchy-LRC matrix builders, lrc.cpp:1511,2140 -- it is host matrix
+ * construction and runs in place on the CPU, with no GPU round trip. */
 int ecg_galois_region_xor(char* src, char* dest, int nbytes);
 /* Replaces jerasure_matrix_encode              (called rs.cpp:24; lrc.cpp:28; erasure_code.cpp:90,109,147) */
 int ecg_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs, int size);

@@ -135,7 +135,7 @@ def test_matrix_dotprod(ecg, oracle, torch_cuda):
 
 
 def test_galois_region_xor(ecg, oracle, torch_cuda):
-    for n in (1, 17, 4096, 100003):
+    for n in (1, 17, 4096, 4097, 100003):  # <= 4096: host coefficient rows; above: the GPU
         s, d = rnd(n, 1), rnd(n, 2)
         d2 = d.copy()
         oracle.galois_region_xor(s, d, n)

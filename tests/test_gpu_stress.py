@@ -133,3 +133,59 @@ def test_thread_per_request_resources_bounded(ecg, oracle):
         assert not any(x.is_alive() for x in th), "a worker hung"
     assert not errors, errors[:5]
     assert ecg.lib().ecg_host_contexts() - before <= 6
+
+
+def test_eviction_does_not_stall_other_streams(ecg, oracle):
+    """Program-cache eviction retires the evicted tables with a completion event per stream they ran on;
+    it does not synchronize the device.  A second stream keeps ~hundreds of ms of encodes queued while
+    this thread evicts on every call: its calls must finish long before that queue drains, and every
+    evicted set is freed once its launches completed."""
+    import time
+
+    import torch
+    saved = ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE)
+    try:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 2)
+        k, m, S, B = 10, 4, 256, 1 << 20
+        M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+        big = torch.empty((S, k + m, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(big, 0xE71C)
+        busy = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        ecg.encode_batch(k, m, M, big[:, :k], big[:, k:], stream=busy.cuda_stream)  # program built up front
+        busy.synchronize()
+        t0 = time.time()
+        ecg.encode_batch(k, m, M, big[:, :k], big[:, k:], stream=busy.cuda_stream)
+        busy.synchronize()
+        one = time.time() - t0
+        reps = max(20, int(0.4 / max(one, 1e-4)))  # ~0.4 s queued on `busy`
+        for _ in range(reps):
+            ecg.encode_batch(k, m, M, big[:, :k], big[:, k:], stream=busy.cuda_stream)
+        rng = np.random.default_rng(7)
+        mine = torch.cuda.Stream()
+        Bs = 4096
+        blocks = torch.from_numpy(rng.integers(0, 256, (6, Bs), dtype=np.uint8)).cuda()
+        torch.cuda.current_stream().synchronize()
+        mats, outs = [], []
+        t0 = time.time()
+        for i in range(24):  # every call a new program: evictions all along
+            Mi = [int(x) for x in rng.integers(1, 256, 4 * 2)]
+            out = torch.zeros((2, Bs), dtype=torch.uint8, device="cuda")
+            ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs,
+                                  stream=mine.cuda_stream)
+            mats.append(Mi)
+            outs.append(out)
+        mine.synchronize()
+        mine_s = time.time() - t0
+        still_busy = not busy.query()
+        busy.synchronize()
+        assert still_busy, f"the busy stream drained first ({reps} x {one * 1e3:.2f} ms queued, evicting calls {mine_s:.3f} s)"
+        host = blocks.cpu().numpy()
+        for Mi, out in zip(mats, outs):
+            want = [np.zeros(Bs, np.uint8) for _ in range(2)]
+            oracle.jerasure_matrix_encode(4, 2, Mi, [host[j] for j in range(4)], want, Bs)
+            assert np.array_equal(out.cpu().numpy(), np.stack(want))
+        torch.cuda.synchronize()
+        assert ecg.lib().ecg_program_sets_retiring() == 0
+    finally:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
