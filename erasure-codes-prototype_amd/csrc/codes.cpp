@@ -59,6 +59,71 @@ void ErasureCode::get_coding_parameters(CodingParameters& cp) const {  // erasur
     cp.local_or_column = local_or_column;
 }
 
+namespace {
+
+uint64_t hash_ints(const std::vector<int>& v) {
+    uint64_t h = 1469598103934665603ull;
+    for (int x : v) h = (h ^ (uint32_t)x) * 1099511628211ull;
+    return h;
+}
+
+template <class V>
+class KeyedCache {
+public:
+    const V* find(const std::vector<int>& key, uint64_t h) const {
+        auto it = map_.find(h);
+        if (it == map_.end()) return nullptr;
+        for (auto& e : it->second)
+            if (e.first == key) return &e.second;
+        return nullptr;
+    }
+    const V& put(std::vector<int> key, uint64_t h, V v) {
+        if (++n_ > kMax) {
+            map_.clear();
+            n_ = 1;
+        }
+        auto& bucket = map_[h];
+        bucket.emplace_back(std::move(key), std::move(v));
+        return bucket.back().second;
+    }
+
+private:
+    static constexpr size_t kMax = 1024;
+    std::unordered_map<uint64_t, std::vector<std::pair<std::vector<int>, V>>> map_;
+    size_t n_ = 0;
+};
+
+}  // namespace
+
+void ErasureCode::state_key(std::vector<int>& key) const {
+    const size_t t = typeid(*this).hash_code();
+    key.insert(key.end(), {(int)(uint32_t)t, (int)(uint32_t)((uint64_t)t >> 32), k, m, w, (int)local_or_column});
+}
+
+void EnlargedRSCode::state_key(std::vector<int>& key) const {
+    RSCode::state_key(key);
+    key.insert(key.end(), {x, seri_num});
+}
+
+void LocallyRepairableCode::state_key(std::vector<int>& key) const {
+    ErasureCode::state_key(key);
+    key.insert(key.end(), {l, g, r});
+}
+
+void ProductCode::state_key(std::vector<int>& key) const {
+    ErasureCode::state_key(key);
+    key.insert(key.end(), {k1, m1, k2, m2});
+    row_code.state_key(key);
+    col_code.state_key(key);
+}
+
+void HPC::state_key(std::vector<int>& key) const {
+    ProductCode::state_key(key);
+    key.push_back((int)isvertical);
+    e_row_code.state_key(key);
+    e_col_code.state_key(key);
+}
+
 void ErasureCode::get_full_matrix(int* matrix, int kk) {  // erasure_code.cpp:30-35
     for (int i = 0; i < kk; i++) matrix[(size_t)i * kk + i] = 1;
 }
@@ -91,6 +156,26 @@ void ErasureCode::partial_decoding_matrix_(int k_, const int* full, const std::v
                                            const std::vector<int>& si, const std::vector<int>& fi,
                                            std::vector<int>& out) {
     const int nl = (int)lsi.size(), nf = (int)fi.size();
+    // memo keyed by everything the result depends on: the ids and the rows of `full` they select
+    thread_local KeyedCache<std::vector<int>> memo;
+    thread_local std::vector<int> key;
+    const size_t ns = si.size(), len = 4 + (size_t)nl + ns + (size_t)nf + (ns + (size_t)nf) * (size_t)k_;
+    key.resize(len);
+    int* w = key.data();
+    *w++ = k_;
+    *w++ = nl;
+    *w++ = (int)ns;
+    *w++ = nf;
+    for (int x : lsi) *w++ = x;
+    for (int x : si) *w++ = x;
+    for (int x : fi) *w++ = x;
+    for (int r : si) w = std::copy(full + (size_t)r * k_, full + (size_t)r * k_ + k_, w);
+    for (int r : fi) w = std::copy(full + (size_t)r * k_, full + (size_t)r * k_ + k_, w);
+    const uint64_t h = hash_ints(key);
+    if (const std::vector<int>* hit = memo.find(key, h)) {
+        out = *hit;
+        return;
+    }
     std::vector<int> fm((size_t)nf * k_, 0), sm((size_t)k_ * k_, 0), inv;
     make_submatrix_by_rows(k_, full, fm.data(), fi);
     make_submatrix_by_rows(k_, full, sm.data(), si);
@@ -108,6 +193,52 @@ void ErasureCode::partial_decoding_matrix_(int k_, const int* full, const std::v
             out[(size_t)u * nl + i] = at < dec.size() ? dec[at] : 0;
         }
     }
+    memo.put(key, h, out);
+}
+
+namespace {
+
+// Per-thread plan caches.  The proxy makes one ErasureCode call per stripe (proxy.cpp:312-349,
+// handle_repair.cpp:249,375), and a batch scope records such a call in ~0.1 us, so rebuilding the
+// call's coefficient matrix (a Gauss-Jordan inversion per partial decode, erasure_code.cpp:113-150) and
+// its plan each time would dominate.  Keys are the exact inputs of the computation (ids and matrix
+// entries), so a hit is the value the computation would return; each cache is bounded and simply
+// cleared when full.
+// jerasure_matrix_encode(kk, mm, matrix) as an interned plan
+SharedOps encode_plan(int kk, int mm, const int* matrix) {
+    thread_local KeyedCache<SharedOps> cache;
+    thread_local std::vector<int> key;
+    key.resize(3 + (size_t)kk * mm);
+    key[0] = 0;
+    key[1] = kk;
+    key[2] = mm;
+    std::copy(matrix, matrix + (size_t)kk * mm, key.begin() + 3);
+    const uint64_t h = hash_ints(key);
+    if (const SharedOps* hit = cache.find(key, h)) return *hit;
+    auto ops = std::make_shared<std::vector<LinearOp>>();
+    LinearOp op = plan_matrix_encode(kk, mm, matrix);
+    if (op.m_out() > 0) ops->push_back(std::move(op));
+    return cache.put(key, h, ops);
+}
+
+}  // namespace
+
+int ErasureCode::run(const SharedOps& ops, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding,
+                     long long B) {
+    if (ops->empty()) return ECG_OK;
+    const int n = n_data + n_coding;
+    uint8_t* small[64];
+    std::vector<uint8_t*> large;
+    uint8_t** blocks = small;
+    if (n > 64) {
+        large.resize((size_t)n);
+        blocks = large.data();
+    }
+    for (int i = 0; i < n_data; i++) blocks[i] = (uint8_t*)data_ptrs[i];
+    for (int i = 0; i < n_coding; i++) blocks[n_data + i] = (uint8_t*)coding_ptrs[i];
+    Engine& eng = Engine::instance();
+    if (mem == ECG_MEM_DEVICE) return eng.run_device(ops, blocks, n, B, stream);
+    return eng.run_host(*ops, blocks, n, B);
 }
 
 int ErasureCode::run(const Plan& plan, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding,
@@ -131,26 +262,21 @@ int ErasureCode::run(const Plan& plan, char** data_ptrs, int n_data, char** codi
 int ErasureCode::run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B,
                             bool stable_matrix) {
     // The encode plan's block ids are already the call's (data 0..kk-1, coding kk..kk+mm-1).  A matrix
-    // from the process-wide builder cache never changes behind its pointer, so its plan is reused
-    // (one entry per thread): the per-stripe call then allocates nothing for planning.
+    // from the process-wide builder cache never changes behind its pointer, so its plan is reused by
+    // pointer (one entry per thread); any other matrix goes through the content-keyed plan cache.
     if (stable_matrix) {
         thread_local const int* last_matrix = nullptr;
         thread_local int last_k = -1, last_m = -1;
-        thread_local Plan last_plan;
+        thread_local SharedOps last_plan;
         if (matrix != last_matrix || kk != last_k || mm != last_m) {
-            last_plan.ops.clear();
-            LinearOp op = plan_matrix_encode(kk, mm, matrix);
-            if (op.m_out() > 0) last_plan.ops.push_back(std::move(op));
+            last_plan = encode_plan(kk, mm, matrix);
             last_matrix = matrix;
             last_k = kk;
             last_m = mm;
         }
         return run(last_plan, data_ptrs, kk, coding_ptrs, mm, B);
     }
-    Plan p;
-    LinearOp op = plan_matrix_encode(kk, mm, matrix);
-    if (op.m_out() > 0) p.ops.push_back(std::move(op));
-    return run(p, data_ptrs, kk, coding_ptrs, mm, B);
+    return run(encode_plan(kk, mm, matrix), data_ptrs, kk, coding_ptrs, mm, B);
 }
 
 int ErasureCode::run_decode(int kk, int mm, const int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
@@ -161,23 +287,53 @@ int ErasureCode::run_decode(int kk, int mm, const int* matrix, int row_k_ones, i
     return run(p, data_ptrs, kk, coding_ptrs, mm, B);
 }
 
+// Per-thread cache of the partial calls' plans, keyed by the object's state_key and the call's index
+// lists: a proxy repairing stripe after stripe repeats the same few patterns, and the matrix behind a
+// partial decode is an inversion.
+static KeyedCache<SharedOps>& partial_plans() {
+    thread_local KeyedCache<SharedOps> cache;
+    return cache;
+}
+
+static void append_list(std::vector<int>& key, const std::vector<int>& v) {
+    key.push_back((int)v.size());
+    key.insert(key.end(), v.begin(), v.end());
+}
+
 int ErasureCode::encode_partial_blocks_for_encoding(char** data_ptrs, char** coding_ptrs, int block_size,
                                                     std::vector<int> data_idxs, std::vector<int> parity_idxs) {
-    std::vector<int> M;
     const int nd = (int)data_idxs.size(), np = (int)parity_idxs.size();
+    thread_local std::vector<int> key;
+    key.assign({2});
+    state_key(key);
+    append_list(key, data_idxs);
+    append_list(key, parity_idxs);
+    const uint64_t h = hash_ints(key);
+    if (const SharedOps* hit = partial_plans().find(key, h)) return run(*hit, data_ptrs, nd, coding_ptrs, np, block_size);
+    std::vector<int> M;
     int rc = partial_encoding_matrix(std::move(data_idxs), std::move(parity_idxs), M);
     if (rc != ECG_OK) return rc;
-    return run_encode(nd, np, M.data(), data_ptrs, coding_ptrs, block_size);
+    const SharedOps plan = partial_plans().put(key, h, encode_plan(nd, np, M.data()));
+    return run(plan, data_ptrs, nd, coding_ptrs, np, block_size);
 }
 
 int ErasureCode::encode_partial_blocks_for_decoding(char** data_ptrs, char** coding_ptrs, int block_size,
                                                     std::vector<int> lsi, std::vector<int> si,
                                                     std::vector<int> fi) {
-    std::vector<int> M;
     const int nl = (int)lsi.size(), nf = (int)fi.size();
+    thread_local std::vector<int> key;
+    key.assign({3});
+    state_key(key);
+    append_list(key, lsi);
+    append_list(key, si);
+    append_list(key, fi);
+    const uint64_t h = hash_ints(key);
+    if (const SharedOps* hit = partial_plans().find(key, h)) return run(*hit, data_ptrs, nl, coding_ptrs, nf, block_size);
+    std::vector<int> M;
     int rc = partial_decoding_matrix(std::move(lsi), std::move(si), std::move(fi), M);
     if (rc != ECG_OK) return rc;
-    return run_encode(nl, nf, M.data(), data_ptrs, coding_ptrs, block_size);
+    const SharedOps plan = partial_plans().put(key, h, encode_plan(nl, nf, M.data()));
+    return run(plan, data_ptrs, nl, coding_ptrs, nf, block_size);
 }
 
 // erasure_code.cpp:70-94: coding[i] = XOR_j data[j * parity_num + i], one launch for all i.
@@ -185,16 +341,21 @@ int ErasureCode::perform_addition(char** data_ptrs, char** coding_ptrs, int bloc
                                   int parity_num) {
     if (parity_num <= 0 || block_num < 0 || block_num % parity_num != 0) return ECG_EINVAL;
     if (block_num == 0) return ECG_OK;
-    LinearOp op;
-    op.src_ids = iota_ids(block_num);
-    op.dst_ids = iota_ids(parity_num, block_num);
-    op.coef.assign((size_t)parity_num * block_num, 0);
-    const int per = block_num / parity_num;
-    for (int i = 0; i < parity_num; i++)
-        for (int j = 0; j < per; j++) op.coef[(size_t)i * block_num + (size_t)j * parity_num + i] = 1;
-    Plan p;
-    p.ops.push_back(std::move(op));
-    return run(p, data_ptrs, block_num, coding_ptrs, parity_num, block_size);
+    thread_local KeyedCache<SharedOps> cache;
+    std::vector<int> key{1, block_num, parity_num};
+    const uint64_t h = hash_ints(key);
+    const SharedOps* plan = cache.find(key, h);
+    if (!plan) {
+        LinearOp op;
+        op.src_ids = iota_ids(block_num);
+        op.dst_ids = iota_ids(parity_num, block_num);
+        op.coef.assign((size_t)parity_num * block_num, 0);
+        const int per = block_num / parity_num;
+        for (int i = 0; i < parity_num; i++)
+            for (int j = 0; j < per; j++) op.coef[(size_t)i * block_num + (size_t)j * parity_num + i] = 1;
+        plan = &cache.put(std::move(key), h, std::make_shared<const std::vector<LinearOp>>(1, std::move(op)));
+    }
+    return run(*plan, data_ptrs, block_num, coding_ptrs, parity_num, block_size);
 }
 
 // out[u] = XOR_i R[u][i] * local[i]  XOR  XOR_j partial[j * nf + u]  (one launch)

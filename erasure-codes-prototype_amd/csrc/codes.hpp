@@ -38,6 +38,7 @@ struct RepairPlan {
 struct Plan {
     std::vector<LinearOp> ops;
 };
+using SharedOps = std::shared_ptr<const std::vector<LinearOp>>;
 
 // Sub-call helpers (ids of the sub-call's data / coding blocks inside the caller's block space).
 void append_encode(Plan& plan, int k, int m, const int* matrix, const std::vector<int>& data_ids,
@@ -94,6 +95,11 @@ public:
 
     virtual std::string self_information() const = 0;
 
+    // Everything the coefficient matrices of this object depend on (class + parameters, sub-codes
+    // included): the key of the per-thread plan cache of the per-call methods.  A class that adds a
+    // matrix-relevant field appends it here.
+    virtual void state_key(std::vector<int>& key) const;
+
     // ---- partitioning and repair planning (planning.cpp)
     int placement_rule = ECG_PLACE_OPTIMAL;  // erasure_code.h:66 default OPTIMAL
     std::vector<std::vector<int>> partition_plan;
@@ -133,6 +139,8 @@ protected:
 
     // Execute a plan over data_ptrs (n_data) ++ coding_ptrs (n_coding) on this object's memory tier.
     int run(const Plan& plan, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding, long long B);
+    // The same with an interned plan (per-thread plan caches below): recorded in a batch scope without a copy.
+    int run(const SharedOps& ops, char** data_ptrs, int n_data, char** coding_ptrs, int n_coding, long long B);
     // jerasure_matrix_encode / _decode over this call's pointers
     int run_encode(int kk, int mm, const int* matrix, char** data_ptrs, char** coding_ptrs, long long B,
                    bool stable_matrix = false);
@@ -181,6 +189,7 @@ public:
     EnlargedRSCode() = default;
     EnlargedRSCode(int k_, int m_) : RSCode(k_, m_) {}
     void init_coding_parameters(const CodingParameters& cp) override;
+    void state_key(std::vector<int>& key) const override;
     int make_encoding_matrix(int* final_matrix) override;
     std::string self_information() const override;
 };
@@ -195,6 +204,7 @@ public:
     }
     void init_coding_parameters(const CodingParameters& cp) override;
     void get_coding_parameters(CodingParameters& cp) const override;
+    void state_key(std::vector<int>& key) const override;
     int encode(char** data_ptrs, char** coding_ptrs, int block_size) override;
     int decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) override;
     int decode_global(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num);
@@ -320,6 +330,7 @@ public:
           k1(k1_), m1(m1_), k2(k2_), m2(m2_) {}
     void init_coding_parameters(const CodingParameters& cp) override;
     void get_coding_parameters(CodingParameters& cp) const override;
+    void state_key(std::vector<int>& key) const override;
     int encode(char** data_ptrs, char** coding_ptrs, int block_size) override;
     int decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) override;
     int check_if_decodable(const std::vector<int>& failure_idxs) override;
@@ -357,6 +368,7 @@ public:
     void init_coding_parameters(const CodingParameters& cp) override;
     int oldbid2newbid_for_merge(int old_block_id, int x, int seri_num, bool isvertical) override;
     std::string self_information() const override;
+    void state_key(std::vector<int>& key) const override;
 
 protected:
     RSCode& rowc() override { return isvertical ? (RSCode&)row_code : (RSCode&)e_row_code; }

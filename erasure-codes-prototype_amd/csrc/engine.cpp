@@ -104,9 +104,40 @@ void set_last_error(const std::string& s) { t_last_error = s; }
 // Freed without waiting: a set that was ever launched is destroyed only by sweep_retired(), after its
 // launches completed; any other (a lost insertion race, a failed build) was never launched.
 ProgramSet::~ProgramSet() {
-    if (d_tabs) (void)hipFree(d_tabs);
-    if (d_src) (void)hipFree(d_src);
-    if (d_dst) (void)hipFree(d_dst);
+    if (mem) owner->release_tables(mem, mem_class);
+}
+
+void* Engine::acquire_tables(size_t bytes, size_t* cls, hipError_t* err) {
+    size_t c = 256;
+    while (c < bytes) c <<= 1;
+    *cls = c;
+    *err = hipSuccess;
+    {
+        std::lock_guard<std::mutex> lk(pmu_);
+        auto it = pool_.find(c);
+        if (it != pool_.end() && !it->second.empty()) {
+            void* p = it->second.back();
+            it->second.pop_back();
+            pooled_bytes_ -= c;
+            return p;
+        }
+    }
+    void* p = nullptr;
+    *err = hipMalloc(&p, c);
+    return *err == hipSuccess ? p : nullptr;
+}
+
+void Engine::release_tables(void* p, size_t cls) {
+    constexpr size_t kPoolCap = 64 << 20;  // beyond this, blocks are freed (rare: a cache of large programs)
+    {
+        std::lock_guard<std::mutex> lk(pmu_);
+        if (pooled_bytes_ + cls <= kPoolCap) {
+            pool_[cls].push_back(p);
+            pooled_bytes_ += cls;
+            return;
+        }
+    }
+    (void)hipFree(p);
 }
 
 void Engine::retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted) {
@@ -245,15 +276,29 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
         return nullptr;
     };
     hipError_t e;
-    if ((e = hipMalloc(&ps->d_tabs, tabs.size() * sizeof(CoefTab))) != hipSuccess) return fail(e, "hipMalloc(tabs)");
-    if ((e = hipMalloc(&ps->d_src, src.size() * sizeof(int))) != hipSuccess) return fail(e, "hipMalloc(src)");
-    if ((e = hipMalloc(&ps->d_dst, dst.size() * sizeof(int))) != hipSuccess) return fail(e, "hipMalloc(dst)");
-    if ((e = hipMemcpy(ps->d_tabs, tabs.data(), tabs.size() * sizeof(CoefTab), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail(e, "hipMemcpy(tabs)");
-    if ((e = hipMemcpy(ps->d_src, src.data(), src.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail(e, "hipMemcpy(src)");
-    if ((e = hipMemcpy(ps->d_dst, dst.data(), dst.size() * sizeof(int), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail(e, "hipMemcpy(dst)");
+    // one device block: tables, then source ids, then destination ids
+    const size_t tab_bytes = tabs.size() * sizeof(CoefTab), src_off = tab_bytes,
+                 dst_off = src_off + ((src.size() * sizeof(int) + 15) & ~(size_t)15),
+                 total = dst_off + dst.size() * sizeof(int);
+    std::vector<uint8_t> host(total, 0);
+    memcpy(host.data(), tabs.data(), tab_bytes);
+    memcpy(host.data() + src_off, src.data(), src.size() * sizeof(int));
+    memcpy(host.data() + dst_off, dst.data(), dst.size() * sizeof(int));
+    ps->owner = this;
+    ps->mem = acquire_tables(total, &ps->mem_class, &e);
+    if (!ps->mem) return fail(e, "hipMalloc(program tables)");
+    ps->d_tabs = (CoefTab*)ps->mem;
+    ps->d_src = (int*)((uint8_t*)ps->mem + src_off);
+    ps->d_dst = (int*)((uint8_t*)ps->mem + dst_off);
+    {
+        // a private non-blocking stream: the upload never waits for (or joins) other streams' work
+        std::lock_guard<std::mutex> lk(pmu_);
+        if (!upload_ && (e = hipStreamCreateWithFlags(&upload_, hipStreamNonBlocking)) != hipSuccess)
+            return fail(e, "hipStreamCreate(upload)");
+        if ((e = hipMemcpyAsync(ps->mem, host.data(), total, hipMemcpyHostToDevice, upload_)) != hipSuccess)
+            return fail(e, "hipMemcpyAsync(program tables)");
+        if ((e = hipStreamSynchronize(upload_)) != hipSuccess) return fail(e, "hipStreamSynchronize(upload)");
+    }
     std::vector<std::shared_ptr<ProgramSet>> evicted;  // retired outside the lock
     {
         std::lock_guard<std::mutex> lk(mu_);
@@ -455,7 +500,8 @@ namespace {
 
 // A linear combination of real blocks over GF(2^8): (block, coefficient) terms, coefficients != 0 once
 // normalised.  Small (a partial repair combines <= k' blocks), so a flat vector.
-using Terms = std::vector<std::pair<uint8_t*, uint8_t>>;
+using Term = std::pair<uint8_t*, uint8_t>;
+using Terms = std::vector<Term>;
 
 void add_term(Terms& t, uint8_t* p, int c) {
     if (!c) return;
@@ -468,204 +514,391 @@ void add_term(Terms& t, uint8_t* p, int c) {
 }
 
 void drop_zero_terms(Terms& t) {
-    t.erase(std::remove_if(t.begin(), t.end(), [](const std::pair<uint8_t*, uint8_t>& x) { return x.second == 0; }),
-            t.end());
+    t.erase(std::remove_if(t.begin(), t.end(), [](const Term& x) { return x.second == 0; }), t.end());
 }
 
-struct Expr {
-    Engine* eng;
-    hipStream_t st;
-    long long B;
-    Terms t;
+// Open-addressing map block address -> int, -1 = absent.  Entries are never erased (set to -1): one flush
+// touches few distinct addresses, and the map lives for one flush.
+class PtrInt {
+public:
+    int get(const void* ptr) const {
+        if (slots_.empty()) return -1;
+        const uintptr_t p = (uintptr_t)ptr;
+        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
+            if (slots_[i].p == p) return slots_[i].v;
+            if (slots_[i].p == 0) return -1;
+        }
+    }
+    int& ref(const void* ptr) {
+        if ((count_ + 1) * 2 > slots_.size()) grow();
+        const uintptr_t p = (uintptr_t)ptr;
+        for (size_t i = hash(p) & mask_;; i = (i + 1) & mask_) {
+            if (slots_[i].p == p) return slots_[i].v;
+            if (slots_[i].p == 0) {
+                slots_[i] = Slot{p, -1};
+                count_++;
+                return slots_[i].v;
+            }
+        }
+    }
+    // empty, with room for n addresses without growing
+    void reset(size_t n) {
+        size_t want = 256;
+        while (want < 4 * n) want <<= 1;
+        if (slots_.size() < want) {
+            slots_.assign(want, Slot{0, -1});
+            mask_ = want - 1;
+        } else if (count_) {
+            std::fill(slots_.begin(), slots_.end(), Slot{0, -1});
+        }
+        count_ = 0;
+    }
+    template <class F>
+    void for_each(F f) const {
+        for (const Slot& s : slots_)
+            if (s.p && s.v >= 0) f((uint8_t*)s.p, s.v);
+    }
+
+private:
+    struct Slot {
+        uintptr_t p;
+        int v;
+    };
+    static size_t hash(uintptr_t p) { return ptr_hash(p); }
+    void grow() {
+        std::vector<Slot> old;
+        old.swap(slots_);
+        slots_.assign(old.empty() ? 256 : old.size() * 2, Slot{0, -1});
+        mask_ = slots_.size() - 1;
+        count_ = 0;
+        for (const Slot& s : old)
+            if (s.p) ref((const void*)s.p) = s.v;
+    }
+    std::vector<Slot> slots_;
+    size_t mask_ = 0, count_ = 0;
 };
 
-// One composed call writing rows[i].first = rows[i].second: inputs in first-appearance order (the same
-// for every stripe of one call pattern, so equal patterns intern to one plan), rows that combine to
-// nothing become a k_in = 0 op (zero bytes, what the sequential calls leave there).
-DeferredCall make_call(Engine* eng, hipStream_t st, long long B, const std::vector<std::pair<uint8_t*, Terms>>& rows) {
-    DeferredCall c{eng, st, B, nullptr, {}};
-    // a block written twice by one op holds its last row (every row reads before any row writes)
-    std::vector<bool> keep(rows.size(), true);
-    for (size_t i = 0; i < rows.size(); i++)
-        for (size_t j = i + 1; j < rows.size() && keep[i]; j++)
-            if (rows[j].first == rows[i].first) keep[i] = false;
-    std::vector<uint8_t*> ins;
-    for (size_t i = 0; i < rows.size(); i++) {
-        if (!keep[i]) continue;
-        const auto& r = rows[i];
-        for (auto& x : r.second)
-            if (std::find(ins.begin(), ins.end(), x.first) == ins.end()) ins.push_back(x.first);
+// compose_scratch's state (engine.hpp).  Expressions live in a slab indexed from `ex_`; `users_` maps a
+// real block to a list of (expression, generation) nodes that read it -- a node whose generation is no
+// longer its slot's is stale.  Composed plans are interned by content, so the flush's plan classes see
+// one plan pointer per distinct composed map.
+class Composer {
+public:
+    std::vector<DeferredCall> out;
+    long long nmat = 0;
+
+    // One Composer per thread, reused by every flush (its tables and buffers keep their capacity).
+    void reset(const ScratchRanges& s, size_t ncalls) {
+        scratch_ = &s;
+        out.clear();
+        out.reserve(ncalls);
+        nmat = 0;
+        slab_used_ = 0;
+        free_.clear();
+        uses_.clear();
+        ex_.reset(ncalls);
+        users_.reset(4 * ncalls);
+        if (plans_.size() > 4096) plans_.clear();  // interned composed plans: bounded
     }
-    const int n = (int)ins.size();
-    auto ops = std::make_shared<std::vector<LinearOp>>();
-    LinearOp full, zero;
-    for (int j = 0; j < n; j++) full.src_ids.push_back(j);
-    c.blocks = ins;
-    for (size_t i = 0; i < rows.size(); i++) {
-        if (!keep[i]) continue;
-        const auto& r = rows[i];
-        const int id = (int)c.blocks.size();
-        c.blocks.push_back(r.first);
-        if (r.second.empty()) {
-            zero.dst_ids.push_back(id);
-            continue;
+
+    void call(DeferredCall&& c) {
+        bool touches = false;
+        for (const LinearOp& op : *c.ops) {
+            for (int id : op.src_ids) touches = touches || ex_.get(c.blocks[id]) >= 0;
+            for (int id : op.dst_ids) touches = touches || scratch_->holds(c.blocks[id], c.B);
         }
-        full.dst_ids.push_back(id);
-        const size_t base = full.coef.size();
-        full.coef.resize(base + (size_t)n, 0);
-        for (auto& x : r.second)
-            full.coef[base + (size_t)(std::find(ins.begin(), ins.end(), x.first) - ins.begin())] = x.second;
+        if (!touches) {
+            // expressions reading blocks this call overwrites go out first, together as one op
+            if (!uses_.empty()) {
+                fast_.clear();
+                start_collect(&fast_, c.eng, c.B);
+                for (const LinearOp& op : *c.ops)
+                    for (int id : op.dst_ids) before_write(c.blocks[id]);
+                collect_ = nullptr;
+                if (fast_.n) emit(c.eng, c.st, c.B, fast_);
+            }
+            out.push_back(std::move(c));
+            return;
+        }
+        for (const LinearOp& op : *c.ops) one_op(c, op);
     }
-    if (full.m_out() > 0) ops->push_back(std::move(full));
-    if (zero.m_out() > 0) ops->push_back(std::move(zero));
-    c.ops = std::move(ops);
-    return c;
-}
+
+    void finish(bool scope_end) {
+        if (scope_end) return;  // unconsumed scratch contents are undefined after the scope
+        std::vector<uint8_t*> left;  // a mid-scope flush leaves memory as the sequential calls would
+        ex_.for_each([&](uint8_t* p, int) { left.push_back(p); });
+        std::sort(left.begin(), left.end());
+        write_out(left);
+    }
+
+private:
+    struct Expr {
+        Engine* eng;
+        hipStream_t st;
+        long long B;
+        uint8_t* self;
+        uint32_t gen;
+        Terms t;
+    };
+    struct Use {
+        int expr;
+        uint32_t gen;
+        int next;
+    };
+    // rows (block, terms) of one op being built; elements keep their capacity across uses
+    struct RowBuf {
+        std::vector<std::pair<uint8_t*, Terms>> v;
+        size_t n = 0;
+        void clear() { n = 0; }
+        Terms& add(uint8_t* d) {
+            if (n == v.size()) v.emplace_back();
+            v[n].first = d;
+            return v[n++].second;
+        }
+    };
+
+    void one_op(const DeferredCall& c, const LinearOp& op) {
+        const int k = op.k_in(), m = op.m_out();
+        // inputs whose expression was recorded on another stream / device / block size are written for
+        // real first -- before any row is built, since writing them out can overwrite blocks other
+        // expressions (and so the rows) read
+        std::vector<uint8_t*> foreign;
+        for (int id : op.src_ids) {
+            const int e = ex_.get(c.blocks[id]);
+            if (e >= 0 && !(slab_[e].eng == c.eng && slab_[e].st == c.st && slab_[e].B == c.B))
+                foreign.push_back(c.blocks[id]);
+        }
+        if (!foreign.empty()) write_out(foreign);
+        if ((int)rows_.size() < m) rows_.resize((size_t)m);
+        for (int p = 0; p < m; p++) {
+            Terms& t = rows_[p];
+            t.clear();
+            for (int j = 0; j < k; j++) {
+                const int cf = op.coef[(size_t)p * k + j];
+                if (!cf) continue;
+                uint8_t* src = c.blocks[op.src_ids[j]];
+                const int e = ex_.get(src);
+                if (e >= 0) {
+                    for (const Term& x : slab_[e].t) add_term(t, x.first, gf::mul(cf, x.second));
+                    continue;
+                }
+                add_term(t, src, cf);
+            }
+            drop_zero_terms(t);
+        }
+        // virtual writes first: a new expression may read a block this same op overwrites, and the real
+        // writes below then write it out (into this op) like any other expression reading it.  A virtual
+        // write leaves d's memory as it is, so expressions reading the real d stay valid.
+        for (int p = 0; p < m; p++) {
+            uint8_t* d = c.blocks[op.dst_ids[p]];
+            if (!scratch_->holds(d, c.B)) continue;
+            int& slot = ex_.ref(d);
+            if (slot < 0) {
+                if (!free_.empty()) {
+                    slot = free_.back();
+                    free_.pop_back();
+                } else {
+                    if (slab_used_ == slab_.size()) slab_.emplace_back();
+                    slot = (int)slab_used_++;
+                }
+            }
+            const int e = slot;
+            Expr& x = slab_[e];
+            x.eng = c.eng;
+            x.st = c.st;
+            x.B = c.B;
+            x.self = d;
+            x.gen = ++gen_;
+            x.t.assign(rows_[p].begin(), rows_[p].end());
+            for (const Term& u : x.t) {
+                int& head = users_.ref(u.first);
+                uses_.push_back(Use{e, x.gen, head});
+                head = (int)uses_.size() - 1;
+            }
+        }
+        real_.clear();
+        start_collect(&real_, c.eng, c.B);
+        for (int p = 0; p < m; p++) {
+            uint8_t* d = c.blocks[op.dst_ids[p]];
+            if (scratch_->holds(d, c.B)) continue;
+            before_write(d);
+            real_.add(d).assign(rows_[p].begin(), rows_[p].end());
+        }
+        collect_ = nullptr;
+        if (real_.n) emit(c.eng, c.st, c.B, real_);
+    }
+
+    // While a call's writes are processed, expressions written out because the call overwrites a block
+    // they read join the call's own op (`collect_`): one op reads every input before it writes any
+    // output, so neither side sees the other's writes (a separate earlier call writing scratch block s
+    // would clobber an s the op itself still reads).
+    void start_collect(RowBuf* rows, Engine* eng, long long B) {
+        collect_ = rows;
+        ceng_ = eng;
+        cB_ = B;
+    }
+
+    void materialise(uint8_t* s) {
+        int& slot = ex_.ref(s);
+        if (slot < 0) return;
+        const int e = slot;
+        slot = -1;
+        Expr& x = slab_[e];
+        const Engine* eng = x.eng;
+        Engine* eng_mut = x.eng;
+        hipStream_t st = x.st;
+        const long long B = x.B;
+        Terms t;
+        t.swap(x.t);
+        x.gen = ++gen_;  // every node still naming this slot is stale now
+        free_.push_back(e);
+        before_write(s);
+        if (collect_ && eng == ceng_ && B == cB_) {
+            collect_->add(s).swap(t);
+        } else {
+            RowBuf one;
+            one.add(s).swap(t);
+            emit(eng_mut, st, B, one);
+        }
+        nmat++;
+    }
+
+    // Top level: write the expressions of `ss` out, with every expression they drag along, as ONE op
+    // (expressions can read each other's real blocks both ways once a scratch block's expression read
+    // its own old contents, so written one by one the second would read the first's new bytes).
+    void write_out(const std::vector<uint8_t*>& ss) {
+        RowBuf& rows = wo_;
+        rows.clear();
+        Engine* eng = nullptr;
+        hipStream_t st = nullptr;
+        long long B = 0;
+        for (uint8_t* s : ss) {
+            const int e = ex_.get(s);
+            if (e < 0) continue;
+            if (!collect_) {
+                eng = slab_[e].eng;
+                st = slab_[e].st;
+                B = slab_[e].B;
+                start_collect(&rows, eng, B);
+            }
+            materialise(s);
+        }
+        collect_ = nullptr;
+        if (rows.n) emit(eng, st, B, rows);
+    }
+
+    // d is about to be overwritten: every expression still reading d is written out first
+    void before_write(uint8_t* d) {
+        if (uses_.empty()) return;
+        const int h = users_.get(d);
+        if (h < 0) return;
+        users_.ref(d) = -1;
+        for (int u = h; u >= 0; u = uses_[u].next) {
+            const Use nd = uses_[u];
+            Expr& x = slab_[nd.expr];
+            if (x.gen != nd.gen) continue;  // stale: the slot was rewritten or written out since
+            for (const Term& t : x.t)
+                if (t.first == d) {
+                    materialise(x.self);
+                    break;
+                }
+        }
+    }
+
+    // One composed call writing rows[i].first = rows[i].second: inputs in first-appearance order (the same
+    // for every stripe of one call pattern, so equal patterns intern to one plan), rows that combine to
+    // nothing become a k_in = 0 op (zero bytes, what the sequential calls leave there).  A block written
+    // twice by one op holds its last row (every row reads before any row writes).
+    void emit(Engine* eng, hipStream_t st, long long B, const RowBuf& buf) {
+        DeferredCall c{eng, st, B, nullptr, {}};
+        const std::pair<uint8_t*, Terms>* rows = buf.v.data();
+        const size_t nrows = buf.n;
+        keep_.assign(nrows, 1);
+        for (size_t i = 0; i < nrows; i++)
+            for (size_t j = i + 1; j < nrows && keep_[i]; j++)
+                if (rows[j].first == rows[i].first) keep_[i] = 0;
+        ins_.clear();
+        for (size_t i = 0; i < nrows; i++)
+            if (keep_[i])
+                for (const Term& x : rows[i].second)
+                    if (std::find(ins_.begin(), ins_.end(), x.first) == ins_.end()) ins_.push_back(x.first);
+        const int n = (int)ins_.size();
+        // content key: n, then per kept row a zero flag or its n coefficients
+        key_.assign((const uint8_t*)&n, (const uint8_t*)&n + sizeof n);
+        c.blocks.reserve(ins_.size() + nrows);
+        c.blocks.assign(ins_.begin(), ins_.end());
+        for (size_t i = 0; i < nrows; i++) {
+            if (!keep_[i]) continue;
+            c.blocks.push_back(rows[i].first);
+            key_.push_back(rows[i].second.empty() ? 0 : 1);
+            if (rows[i].second.empty()) continue;
+            const size_t base = key_.size();
+            key_.resize(base + (size_t)n, 0);
+            for (const Term& x : rows[i].second)
+                key_[base + (size_t)(std::find(ins_.begin(), ins_.end(), x.first) - ins_.begin())] = x.second;
+        }
+        uint64_t h = 1469598103934665603ull;
+        for (uint8_t b : key_) h = (h ^ b) * 1099511628211ull;
+        auto& bucket = plans_[h];
+        for (auto& pl : bucket)
+            if (pl.first == key_) {
+                c.ops = pl.second;
+                out.push_back(std::move(c));
+                return;
+            }
+        auto ops = std::make_shared<std::vector<LinearOp>>();
+        LinearOp full, zero;
+        for (int j = 0; j < n; j++) full.src_ids.push_back(j);
+        int id = n;
+        size_t at = sizeof n;
+        for (size_t i = 0; i < nrows; i++) {
+            if (!keep_[i]) continue;
+            const bool nz = key_[at++];
+            if (!nz) {
+                zero.dst_ids.push_back(id++);
+                continue;
+            }
+            full.dst_ids.push_back(id++);
+            full.coef.insert(full.coef.end(), key_.begin() + (long)at, key_.begin() + (long)at + n);
+            at += (size_t)n;
+        }
+        if (full.m_out() > 0) ops->push_back(std::move(full));
+        if (zero.m_out() > 0) ops->push_back(std::move(zero));
+        c.ops = ops;
+        bucket.emplace_back(key_, std::move(ops));
+        out.push_back(std::move(c));
+    }
+
+    const ScratchRanges* scratch_ = nullptr;
+    std::vector<Expr> slab_;
+    size_t slab_used_ = 0;
+    std::vector<int> free_;
+    PtrInt ex_, users_;
+    std::vector<Use> uses_;
+    uint32_t gen_ = 0;
+    RowBuf* collect_ = nullptr;
+    RowBuf real_, fast_, wo_;
+    const Engine* ceng_ = nullptr;
+    long long cB_ = 0;
+    std::vector<Terms> rows_;
+    std::vector<uint8_t*> ins_;
+    std::vector<char> keep_;
+    std::vector<uint8_t> key_;
+    std::unordered_map<uint64_t, std::vector<std::pair<std::vector<uint8_t>, std::shared_ptr<const std::vector<LinearOp>>>>>
+        plans_;
+};
 
 }  // namespace
 
 std::vector<DeferredCall> compose_scratch(std::vector<DeferredCall>&& q, const ScratchRanges& scratch, bool scope_end,
                                           long long* materialised) {
+    thread_local Composer cp;
+    cp.reset(scratch, q.size());
+    for (DeferredCall& c : q) cp.call(std::move(c));
+    cp.finish(scope_end);
+    if (materialised) *materialised = cp.nmat;
     std::vector<DeferredCall> out;
-    out.reserve(q.size());
-    std::unordered_map<uint8_t*, Expr> ex;                     // scratch block -> what it holds
-    std::unordered_map<uint8_t*, std::vector<uint8_t*>> users;  // real block -> scratch blocks whose expr reads it
-    long long nmat = 0;
-    // While a call's writes are processed, expressions written out because the call overwrites a block
-    // they read join the call's own op (`collect`): one op reads every input before it writes any
-    // output, so neither side sees the other's writes (a separate earlier call writing scratch block s
-    // would clobber an s the op itself still reads).
-    std::vector<std::pair<uint8_t*, Terms>>* collect = nullptr;
-    Engine* collect_eng = nullptr;
-    long long collect_B = 0;
-    std::function<void(uint8_t*)> before_write;
-    auto materialise = [&](uint8_t* s) {
-        auto it = ex.find(s);
-        if (it == ex.end()) return;
-        Expr e = std::move(it->second);
-        ex.erase(it);
-        before_write(s);
-        if (collect && e.eng == collect_eng && e.B == collect_B) collect->emplace_back(s, std::move(e.t));
-        else out.push_back(make_call(e.eng, e.st, e.B, {{s, std::move(e.t)}}));
-        nmat++;
-    };
-    // Top level: write the expressions of `ss` out, with every expression they drag along, as ONE op
-    // (expressions can read each other's real blocks both ways once a scratch block's expression read
-    // its own old contents, so written one by one the second would read the first's new bytes).
-    auto write_out = [&](const std::vector<uint8_t*>& ss) {
-        std::vector<std::pair<uint8_t*, Terms>> rows;
-        Engine* eng = nullptr;
-        hipStream_t st = nullptr;
-        long long B = 0;
-        for (uint8_t* s : ss) {
-            auto it = ex.find(s);
-            if (it == ex.end()) continue;
-            if (!collect) {
-                eng = collect_eng = it->second.eng;
-                st = it->second.st;
-                B = collect_B = it->second.B;
-                collect = &rows;
-            }
-            materialise(s);
-        }
-        collect = nullptr;
-        if (!rows.empty()) out.push_back(make_call(eng, st, B, rows));
-    };
-    // d is about to be overwritten: every expression still reading d is written out first
-    before_write = [&](uint8_t* d) {
-        auto u = users.find(d);
-        if (u == users.end()) return;
-        std::vector<uint8_t*> v = std::move(u->second);
-        users.erase(u);
-        for (uint8_t* s : v) {
-            auto it = ex.find(s);
-            if (it == ex.end()) continue;
-            for (auto& x : it->second.t)
-                if (x.first == d) {
-                    materialise(s);
-                    break;
-                }
-        }
-    };
-    for (DeferredCall& c : q) {
-        bool touches = false;
-        for (const LinearOp& op : *c.ops) {
-            for (int id : op.src_ids) touches = touches || ex.count(c.blocks[id]);
-            for (int id : op.dst_ids) touches = touches || scratch.holds(c.blocks[id], c.B);
-        }
-        if (!touches) {
-            // expressions reading blocks this call overwrites go out first, together as one op
-            std::vector<std::pair<uint8_t*, Terms>> rows;
-            if (!users.empty()) {
-                collect = &rows;
-                collect_eng = c.eng;
-                collect_B = c.B;
-                for (const LinearOp& op : *c.ops)
-                    for (int id : op.dst_ids) before_write(c.blocks[id]);
-                collect = nullptr;
-            }
-            if (!rows.empty()) out.push_back(make_call(c.eng, c.st, c.B, rows));
-            out.push_back(std::move(c));
-            continue;
-        }
-        for (const LinearOp& op : *c.ops) {
-            const int k = op.k_in(), m = op.m_out();
-            // inputs whose expression was recorded on another stream / device / block size are written
-            // for real first -- before any row is built, since writing them out can overwrite blocks
-            // other expressions (and so the rows) read
-            std::vector<uint8_t*> foreign;
-            for (int id : op.src_ids) {
-                auto it = ex.find(c.blocks[id]);
-                if (it != ex.end() && !(it->second.eng == c.eng && it->second.st == c.st && it->second.B == c.B))
-                    foreign.push_back(c.blocks[id]);
-            }
-            if (!foreign.empty()) write_out(foreign);
-            std::vector<std::pair<uint8_t*, Terms>> rows((size_t)m);
-            for (int p = 0; p < m; p++) {
-                Terms& t = rows[p].second;
-                for (int j = 0; j < k; j++) {
-                    const int cf = op.coef[(size_t)p * k + j];
-                    if (!cf) continue;
-                    uint8_t* src = c.blocks[op.src_ids[j]];
-                    auto it = ex.find(src);
-                    if (it != ex.end()) {
-                        for (auto& x : it->second.t) add_term(t, x.first, gf::mul(cf, x.second));
-                        continue;
-                    }
-                    add_term(t, src, cf);
-                }
-                drop_zero_terms(t);
-            }
-            std::vector<std::pair<uint8_t*, Terms>> real;
-            collect = &real;
-            collect_eng = c.eng;
-            collect_B = c.B;
-            // virtual writes first: a new expression may read a block this same op overwrites, and the
-            // real writes below then write it out (into this op) like any other expression reading it.
-            // A virtual write leaves d's memory as it is, so expressions reading the real d stay valid.
-            for (int p = 0; p < m; p++) {
-                uint8_t* d = c.blocks[op.dst_ids[p]];
-                if (!scratch.holds(d, c.B)) continue;
-                for (auto& x : rows[p].second) users[x.first].push_back(d);
-                ex[d] = Expr{c.eng, c.st, c.B, std::move(rows[p].second)};
-            }
-            for (int p = 0; p < m; p++) {
-                uint8_t* d = c.blocks[op.dst_ids[p]];
-                if (scratch.holds(d, c.B)) continue;
-                before_write(d);
-                real.emplace_back(d, std::move(rows[p].second));
-            }
-            collect = nullptr;
-            if (!real.empty()) out.push_back(make_call(c.eng, c.st, c.B, real));
-        }
-    }
-    if (!scope_end && !ex.empty()) {  // a mid-scope flush leaves memory as the sequential calls would
-        std::vector<uint8_t*> left;
-        for (auto& kv : ex) left.push_back(kv.first);
-        std::sort(left.begin(), left.end());
-        write_out(left);
-    }
-    if (materialised) *materialised = nmat;
+    out.swap(cp.out);
     return out;
 }
 
@@ -851,15 +1084,20 @@ int Engine::launch_direct(const std::vector<LinearOp>& ops, uint8_t* const* bloc
     return ECG_OK;
 }
 
-int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B,
-                       hipStream_t st) {
-    if (B < 0) return ECG_EINVAL;
+static int check_ids(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks) {
     for (const LinearOp& op : ops) {
         for (int id : op.src_ids)
             if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
         for (int id : op.dst_ids)
             if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
     }
+    return ECG_OK;
+}
+
+int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B,
+                       hipStream_t st) {
+    if (B < 0) return ECG_EINVAL;
+    if (const int rc = check_ids(ops, blocks, nblocks); rc != ECG_OK) return rc;
     if (t_defer.active) {
         if (ops.empty() || B == 0) return ECG_OK;
         std::shared_ptr<const std::vector<LinearOp>> shared;
@@ -869,6 +1107,18 @@ int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks,
         return t_defer.q.size() >= kMaxDeferred ? batch_flush() : ECG_OK;
     }
     return launch_direct(ops, blocks, B, st);
+}
+
+int Engine::run_device(const std::shared_ptr<const std::vector<LinearOp>>& ops, uint8_t* const* blocks, int nblocks,
+                       long long B, hipStream_t st) {
+    if (B < 0 || !ops) return ECG_EINVAL;
+    if (const int rc = check_ids(*ops, blocks, nblocks); rc != ECG_OK) return rc;
+    if (t_defer.active) {  // recorded with the caller's (interned) plan: no copy
+        if (ops->empty() || B == 0) return ECG_OK;
+        t_defer.q.push_back(DeferredCall{this, st, B, ops, std::vector<uint8_t*>(blocks, blocks + nblocks)});
+        return t_defer.q.size() >= kMaxDeferred ? batch_flush() : ECG_OK;
+    }
+    return launch_direct(*ops, blocks, B, st);
 }
 
 // Host-buffer tier (the reference's per-stripe calls on host memory).  Device slots are assigned to the

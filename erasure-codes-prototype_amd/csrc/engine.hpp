@@ -34,7 +34,12 @@ namespace ecg {
 constexpr size_t kStagedMaxBlock = 256 << 10;
 constexpr size_t kStagedMaxBytes = 8 << 20;
 
+class Engine;
+
 struct ProgramSet {
+    Engine* owner = nullptr;  // its device memory (one block: tables + ids) goes back to owner's pool
+    void* mem = nullptr;
+    size_t mem_class = 0;
     CoefTab* d_tabs = nullptr;
     int* d_src = nullptr;
     int* d_dst = nullptr;
@@ -54,7 +59,7 @@ struct ProgramSet {
         if (nstreams < kMaxStreams) streams[nstreams++] = s;
         else overflow = true;
     }
-    ~ProgramSet();  // frees at once: only reached when no launch can still read the tables
+    ~ProgramSet();  // returns the memory at once: only reached when no launch can still read the tables
 };
 
 class Engine {
@@ -63,6 +68,9 @@ public:
 
     int run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B,
                    hipStream_t stream);
+    // The same with a shared (interned) plan: a call recorded in a batch scope keeps the pointer.
+    int run_device(const std::shared_ptr<const std::vector<LinearOp>>& ops, uint8_t* const* blocks, int nblocks,
+                   long long B, hipStream_t stream);
     int run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B);
     int run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of_stripe, int S,
                     const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
@@ -101,6 +109,12 @@ private:
     // launched on has fired.  Swept on every cache miss; no device-wide synchronize on this path.
     void retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted);
     void sweep_retired();
+    // Device memory of program tables comes from a pool of power-of-two blocks, so a steady stream of new
+    // programs (a proxy's open set of repair matrices) neither allocates nor frees device memory --
+    // hipFree synchronizes the device.  Uploads go through a private non-blocking stream.
+    void* acquire_tables(size_t bytes, size_t* cls, hipError_t* err);
+    void release_tables(void* p, size_t cls);
+    friend struct ProgramSet;
 
     int device_;
     struct CacheEntry {
@@ -117,6 +131,10 @@ private:
     };
     std::mutex rmu_;
     std::vector<Retired> retired_;
+    std::mutex pmu_;
+    std::unordered_map<size_t, std::vector<void*>> pool_;
+    size_t pooled_bytes_ = 0;
+    hipStream_t upload_ = nullptr;
 
 public:
     size_t retired_pending();  // evicted sets not yet freed (tests)
@@ -189,6 +207,18 @@ private:
 std::vector<DeferredCall> compose_scratch(std::vector<DeferredCall>&& q, const ScratchRanges& scratch,
                                           bool scope_end, long long* materialised);
 
+// Block addresses are often aligned to the block size (1 MiB and up): a full 64-bit mix (splitmix64's
+// finaliser) so that their low bits, which pick the slot, are not mostly zero.
+inline size_t ptr_hash(uintptr_t p) {
+    unsigned long long x = (unsigned long long)p;
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return (size_t)x;
+}
+
 // Open-addressing map block address -> the latest group (index + 1) that read / wrote it, for the
 // flush's scheduler.  0 = never touched.
 class PtrGroups {
@@ -209,6 +239,18 @@ public:
             }
         }
     }
+    // empty, with room for n addresses without growing (the flush's scheduler reuses one per thread)
+    void reset(size_t n) {
+        size_t want = 1024;
+        while (want < 4 * n) want <<= 1;
+        if (slots_.size() < want) {
+            slots_.assign(want, Slot{0, 0, 0});
+            mask_ = want - 1;
+        } else if (count_) {
+            std::fill(slots_.begin(), slots_.end(), Slot{0, 0, 0});
+        }
+        count_ = 0;
+    }
     int last_write(const void* ptr) const { const Slot* s = find(ptr); return s ? s->wr : 0; }
     int last_touch(const void* ptr) const { const Slot* s = find(ptr); return s ? std::max(s->rd, s->wr) : 0; }
 
@@ -221,7 +263,7 @@ private:
             if (slots_[i].p == 0) return nullptr;
         }
     }
-    static size_t hash(uintptr_t p) { return (size_t)(((unsigned long long)p >> 4) * 0x9E3779B97F4A7C15ull >> 17); }
+    static size_t hash(uintptr_t p) { return ptr_hash(p); }
     void grow() {
         std::vector<Slot> old;
         old.swap(slots_);
@@ -249,7 +291,8 @@ template <class Key, class Reads, class Writes>
 std::vector<std::vector<size_t>> schedule_groups(size_t n, Key key, Reads reads, Writes writes) {
     std::vector<std::vector<size_t>> groups;
     std::vector<int> last_of_key;  // key -> latest group index + 1
-    PtrGroups seen;
+    thread_local PtrGroups seen;
+    seen.reset(4 * n);
     for (size_t c = 0; c < n; c++) {
         int lo = 0;  // the call must go into a group with index + 1 > lo
         reads(c, [&](const void* p) { lo = std::max(lo, seen.last_write(p)); });

@@ -254,6 +254,58 @@ def test_facade_partials_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
             assert same(da, db), ("dec", local, lsub, surv, lost)
 
 
+def test_partial_plan_cache_tells_objects_apart(ecg, oracle, torch_cuda):
+    """The per-thread plan cache of the partial calls is keyed by each object's state (class, parameters,
+    sub-codes): objects of one class that differ only in a parameter the matrices depend on -- ERS
+    seri_num, HPC isvertical, RS vs ERS with the same k and m -- alternate on one thread with identical
+    index lists, and every result must still be its own object's (oracle)."""
+    from oracle import ec_ref as E
+    B = 512
+    pairs = [(1, dict(k=4, m=2, x=2, seri_num=0), dict(k=4, m=2, x=2, seri_num=1)),
+             (1, dict(k=4, m=2, x=2, seri_num=1), dict(k=4, m=2, x=3, seri_num=1)),
+             (0, dict(k=4, m=2), None),  # RS vs ERS(4, 2, x=2, seri_num=1) below
+             (8, dict(k1=2, m1=2, k2=2, m2=1, x=2, seri_num=1), "vertical")]
+    for t, pa, pb in pairs:
+        if pb is None:
+            objs = [(0, pa, None), (1, dict(k=4, m=2, x=2, seri_num=1), None)]
+        elif pb == "vertical":
+            objs = [(t, pa, True), (t, pa, False)]
+        else:
+            objs = [(t, pa, None), (t, pb, None)]
+        built = []
+        for tt, pp, vert in objs:
+            o = E.ec_factory(tt, E.CodingParameters(**pp))
+            p = ecg.ec_factory(tt, ecg.CodingParameters(**pp))
+            p.init_coding_parameters(ecg.CodingParameters(**pp))
+            o.init_coding_parameters(E.CodingParameters(**pp))
+            if vert is not None:
+                o.isvertical = vert
+                p.set_isvertical(vert)
+            built.append((o, p))
+        o0 = built[0][0]
+        k, m = o0.k, o0.m
+        if t >= 7:  # product code: one row of the grid
+            members = [o0.rowcol2bid(0, c) for c in range(o0.k1 + o0.m1)]
+            d_all, par = members[:o0.k1], members[o0.k1:]
+        else:
+            d_all, par = list(range(k)), list(range(k, k + m))
+        sub = d_all[1:]
+        lost = [d_all[0]]
+        surv = (d_all[1:] + par)[:len(d_all)]
+        for rep in range(3):  # alternate: a stale cache entry would hand one object the other's plan
+            for o, p in built:
+                stripe = E.blocks(k, B, 11) + E.zeros(m, B)
+                o.encode(stripe[:k], stripe[k:], B)
+                a, b = E.zeros(len(par), B), E.zeros(len(par), B)
+                o.encode_partial_blocks_for_encoding([stripe[i] for i in sub], a, B, sub, par)
+                p.encode_partial_blocks_for_encoding([stripe[i] for i in sub], b, B, sub, par)
+                assert same(a, b), (t, rep, "enc")
+                da, db = E.zeros(1, B), E.zeros(1, B)
+                o.encode_partial_blocks_for_decoding([stripe[i] for i in surv[:2]], da, B, surv[:2], surv, lost)
+                p.encode_partial_blocks_for_decoding([stripe[i] for i in surv[:2]], db, B, surv[:2], surv, lost)
+                assert same(da, db), (t, rep, "dec")
+
+
 @pytest.mark.parametrize("t,params,local", [(0, dict(k=10, m=4), False), (0, dict(k=6, m=4), False),
                                              (2, dict(k=12, l=2, g=2), True), (2, dict(k=12, l=2, g=2), False)])
 def test_main_repair_with_addition(ecg, oracle, torch_cuda, t, params, local):
@@ -1108,7 +1160,7 @@ def test_batch_scope_scratch_mid_scope_flush_and_streams(ecg, torch_cuda):
         for s, (e, surv, sets) in enumerate(plan):
             for i in range(2):
                 ec.encode_partial_blocks_for_decoding([st[s, b] for b in sets[i]], [partials[s, i]], B, sets[i], surv, [e])
-        ec.perform_addition([partials[0, 0], partials[0, 1]], [out[0]], B, 2, 1, stream=side)
+        ec.perform_addition([partials[0, 0], partials[0, 1]], [out[0]], B, 2, 1, stream=side.cuda_stream)
     torch.cuda.synchronize()
     assert torch.equal(out[0], ref_o[0])
     assert torch.equal(partials[0], ref_p[0])

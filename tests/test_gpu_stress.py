@@ -165,16 +165,13 @@ def test_eviction_does_not_stall_other_streams(ecg, oracle):
         mine = torch.cuda.Stream()
         Bs = 4096
         blocks = torch.from_numpy(rng.integers(0, 256, (6, Bs), dtype=np.uint8)).cuda()
-        torch.cuda.current_stream().synchronize()
-        mats, outs = [], []
+        mats = [[int(x) for x in rng.integers(1, 256, 4 * 2)] for _ in range(24)]
+        outs = [torch.zeros((2, Bs), dtype=torch.uint8, device="cuda") for _ in mats]
+        torch.cuda.current_stream().synchronize()  # inputs and zeroed outputs ready before `mine` runs
         t0 = time.time()
-        for i in range(24):  # every call a new program: evictions all along
-            Mi = [int(x) for x in rng.integers(1, 256, 4 * 2)]
-            out = torch.zeros((2, Bs), dtype=torch.uint8, device="cuda")
+        for Mi, out in zip(mats, outs):  # every call a new program: evictions all along
             ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs,
                                   stream=mine.cuda_stream)
-            mats.append(Mi)
-            outs.append(out)
         mine.synchronize()
         mine_s = time.time() - t0
         still_busy = not busy.query()

@@ -6,9 +6,10 @@ R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out/scope
 O=$R/gpurun_out/scope
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread \
-  -k "batch_scope or galois_region_xor" > $O/pytest.log 2>&1 && timeout -k 10 300 python -u -m pytest tests/test_gpu_stress.py -v -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread -k eviction >> $O/pytest.log 2>&1
-rc=$?; echo "pytest rc=$rc"; grep -E "PASS|FAIL|ERROR" $O/pytest.log | tail -14; [ $rc -eq 0 ] || exit $rc
+if [ -z "${SKIP_TESTS:-}" ]; then
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed" $O/pytest.log | tail -14; [ $rc -eq 0 ] || exit $rc
+fi
 timeout -k 10 300 tools/scope_repair $((1<<20)) 4096 5 512 > $O/scope_repair.log 2>&1
 rc=$?; echo "scope_repair rc=$rc"; cat $O/scope_repair.log; [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp

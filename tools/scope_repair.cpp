@@ -64,16 +64,25 @@ static Repair local_repair(int e) {
     const std::vector<int>* mine = nullptr;
     for (auto& p : parts)
         if (std::count(p.begin(), p.end(), e)) mine = &p;
+    std::vector<int> own;
+    std::vector<std::vector<int>> sets;  // helper partitions' survivors, then the main proxy's own
     for (int b : r.surv)
-        if (std::count(mine->begin(), mine->end(), b)) r.main_.push_back(b);
+        if (std::count(mine->begin(), mine->end(), b)) own.push_back(b);
     for (auto& p : parts) {
         if (&p == mine) continue;
         std::vector<int> in;
         for (int b : r.surv)
             if (std::count(p.begin(), p.end(), b)) in.push_back(b);
-        if (in.size() > 1) r.helper = in;
-        else r.main_.insert(r.main_.end(), in.begin(), in.end());
+        if (in.size() > 1) sets.push_back(in);  // a helper sends one partial (handle_repair.cpp:169-176)
+        else own.insert(own.end(), in.begin(), in.end());
     }
+    if (!own.empty()) sets.push_back(own);
+    if (sets.size() != 2) {
+        fprintf(stderr, "unexpected split for block %d\n", e);
+        exit(1);
+    }
+    r.helper = sets[0];
+    r.main_ = sets[1];
     return r;
 }
 
@@ -128,7 +137,7 @@ int main(int argc, char** argv) {
         OK(ecg_ec_encode_partial_blocks_for_decoding(ec, d.data(), &o, (int)B, r.surv.data(), (int)r.surv.size(),
                                                      r.surv.data(), (int)r.surv.size(), &r.e, 1));
     };
-    // check: out[s] == lost block, on a sample of stripes (every pattern) + a device-wide sum
+    // check: out[s] == lost block, on the first 28 stripes (every pattern twice) and the last
     std::vector<uint8_t> h_out(B), h_want(B);
     auto check = [&](const char* name) {
         CK(hipStreamSynchronize(st));
