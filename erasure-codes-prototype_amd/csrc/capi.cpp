@@ -142,12 +142,13 @@ int ecg_galois_region_xor(char* src, char* dest, int nbytes) {
 
 int ecg_jerasure_matrix_encode(int k, int m, int w, int* matrix, char** data_ptrs, char** coding_ptrs, int size) {
     if (w != 8 || k < 1 || m < 1 || !matrix || !data_ptrs || !coding_ptrs || size < 0) return ECG_EINVAL;
-    LinearOp op = plan_matrix_encode(k, m, matrix);
-    if (op.m_out() == 0) return ECG_OK;
-    std::vector<uint8_t*> blocks((size_t)k + m);
+    const auto plan = encode_plan_cached(k, m, matrix);
+    if (plan->empty()) return ECG_OK;
+    thread_local std::vector<uint8_t*> blocks;
+    blocks.resize((size_t)k + m);
     for (int i = 0; i < k; i++) blocks[i] = (uint8_t*)data_ptrs[i];
     for (int i = 0; i < m; i++) blocks[(size_t)k + i] = (uint8_t*)coding_ptrs[i];
-    return Engine::instance().run_host({op}, blocks.data(), k + m, size);
+    return Engine::instance().run_host(*plan, blocks.data(), k + m, size);
 }
 
 int ecg_jerasure_matrix_dotprod(int k, int w, int* matrix_row, int* src_ids, int dest_id, char** data_ptrs,

@@ -204,22 +204,8 @@ namespace {
 // its plan each time would dominate.  Keys are the exact inputs of the computation (ids and matrix
 // entries), so a hit is the value the computation would return; each cache is bounded and simply
 // cleared when full.
-// jerasure_matrix_encode(kk, mm, matrix) as an interned plan
-SharedOps encode_plan(int kk, int mm, const int* matrix) {
-    thread_local KeyedCache<SharedOps> cache;
-    thread_local std::vector<int> key;
-    key.resize(3 + (size_t)kk * mm);
-    key[0] = 0;
-    key[1] = kk;
-    key[2] = mm;
-    std::copy(matrix, matrix + (size_t)kk * mm, key.begin() + 3);
-    const uint64_t h = hash_ints(key);
-    if (const SharedOps* hit = cache.find(key, h)) return *hit;
-    auto ops = std::make_shared<std::vector<LinearOp>>();
-    LinearOp op = plan_matrix_encode(kk, mm, matrix);
-    if (op.m_out() > 0) ops->push_back(std::move(op));
-    return cache.put(key, h, ops);
-}
+// jerasure_matrix_encode(kk, mm, matrix) as an interned plan (matrix.hpp)
+SharedOps encode_plan(int kk, int mm, const int* matrix) { return encode_plan_cached(kk, mm, matrix); }
 
 }  // namespace
 

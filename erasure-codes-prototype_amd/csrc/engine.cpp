@@ -212,8 +212,12 @@ size_t Engine::cache_size() {
 }
 
 std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& progs, int* status) {
+    return program_set(progs.data(), progs.size(), status);
+}
+
+std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t nprogs, int* status) {
     *status = ECG_OK;
-    if (progs.empty()) {
+    if (nprogs == 0) {
         *status = ECG_EINVAL;
         return nullptr;
     }
@@ -222,15 +226,17 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
         *status = ECG_EINVAL;
         return nullptr;
     }
-    std::string key;
-    key.reserve(16 + progs.size() * (size_t)(k * m + 4 * (k + m)));
+    thread_local std::string key;  // per thread: no allocation per lookup
+    key.clear();
+    key.reserve(16 + nprogs * (size_t)(k * m + 4 * (k + m)));
     auto put = [&](const void* p, size_t n) { key.append((const char*)p, n); };
-    const int np = (int)progs.size();
+    const int np = (int)nprogs;
     put(&k, 4);
     put(&m, 4);
     put(&np, 4);
     bool binary = true;
-    for (const LinearOp& op : progs) {
+    for (size_t pi = 0; pi < nprogs; pi++) {
+        const LinearOp& op = progs[pi];
         if (op.k_in() != k || op.m_out() != m || op.coef.size() != (size_t)k * m) {
             *status = ECG_EINVAL;
             return nullptr;
@@ -324,7 +330,7 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
                 }
             }
         }
-        cache_.emplace(std::move(key), CacheEntry{ps, ++tick_});
+        cache_.emplace(key, CacheEntry{ps, ++tick_});
     }
     if (!evicted.empty()) retire(std::move(evicted));
     sweep_retired();
@@ -334,7 +340,7 @@ std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& pro
 // One op over block pointers (device addresses), any k_in / m_out.  Ops that fit the kernel arguments
 // carry their pointers inline; wider ones (k_in > 128 or m_out > 32) go through an uploaded pointer
 // table (run_ptr_batch with one call), still asynchronous.
-int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st) {
+int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st, bool latency) {
     if (op.m_out() == 0 || B == 0) return ECG_OK;
     if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
         for (int d : op.dst_ids) ECG_HIP(hipMemsetAsync(blocks[d], 0, (size_t)B, st));
@@ -342,7 +348,7 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     }
     if (op.k_in() > kInlineSrc || op.m_out() > kInlineDst) return run_ptr_batch(op, {blocks}, B, st);
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set({op}, &status);
+    std::shared_ptr<ProgramSet> ps = program_set(&op, 1, &status);
     if (!ps) return status;
     GfLaunch a;
     memset(&a, 0, sizeof(a));
@@ -362,7 +368,7 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     for (int j = 0; j < op.k_in(); j++) a.isrc[j] = blocks[op.src_ids[j]];
     for (int p = 0; p < op.m_out(); p++) a.idst[p] = blocks[op.dst_ids[p]];
     ps->used_on(st);
-    ECG_HIP(launch_gf(a, GF_MODE_INLINE, vec_ok, st));
+    ECG_HIP(launch_gf(a, latency ? GF_MODE_INLINE_LAT : GF_MODE_INLINE, vec_ok, st));
     return ECG_OK;
 }
 
@@ -1138,9 +1144,16 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
     HostCtx& c = *lease;
     if (!c.stream) ECG_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     hipStream_t st = c.stream;
-    std::vector<char> upload(nblocks, 0), written(nblocks, 0), used(nblocks, 0);
+    // per-call bookkeeping in per-thread buffers (a 1 KiB call costs ~10 us of which the host's share is
+    // what allocation would add to)
+    thread_local std::vector<char> upload, written, used, produced;
+    thread_local std::vector<int> slot;
+    thread_local std::vector<uint8_t*> dev;
+    upload.assign(nblocks, 0);
+    written.assign(nblocks, 0);
+    used.assign(nblocks, 0);
     {
-        std::vector<char> produced(nblocks, 0);
+        produced.assign(nblocks, 0);
         for (const LinearOp& op : ops) {
             for (int id : op.src_ids) {
                 if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
@@ -1153,7 +1166,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
             }
         }
     }
-    std::vector<int> slot(nblocks, -1);
+    slot.assign(nblocks, -1);
     int nslots = 0, n_up = 0;
     for (int id = 0; id < nblocks; id++)
         if (upload[id]) slot[id] = nslots++;
@@ -1169,7 +1182,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         ECG_HIP(hipMalloc(&c.scratch, pitch * nslots));
         c.cap = pitch * nslots;
     }
-    std::vector<uint8_t*> dev(nblocks, nullptr);
+    dev.assign(nblocks, nullptr);
     for (int id = 0; id < nblocks; id++)
         if (slot[id] >= 0) dev[id] = c.scratch + (size_t)slot[id] * pitch;
     const bool staged = (size_t)B <= kStagedMaxBlock && pitch * nslots <= kStagedMaxBytes;
@@ -1192,7 +1205,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
             if (upload[id]) memcpy(c.pinned + (size_t)slot[id] * pitch, blocks[id], (size_t)B);
         }
         for (const LinearOp& op : ops) {
-            int rc = launch_one(op, dev.data(), B, st);
+            int rc = launch_one(op, dev.data(), B, st, /*latency=*/true);
             if (rc != ECG_OK) {
                 (void)hipStreamSynchronize(st);
                 return rc;
@@ -1316,7 +1329,7 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
     if (S == 0 || B == 0) return ECG_OK;
     if (!d_src || !d_dst) return ECG_EINVAL;
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set({prog}, &status);
+    std::shared_ptr<ProgramSet> ps = program_set(&prog, 1, &status);
     if (!ps) return status;
     GfLaunch a;
     memset(&a, 0, sizeof(a));
@@ -1376,7 +1389,7 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     for (int j = 0; j < kin; j++) dev.src_ids[j] = j;
     for (int p = 0; p < mout; p++) dev.dst_ids[p] = p;
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set({dev}, &status);
+    std::shared_ptr<ProgramSet> ps = program_set(&dev, 1, &status);
     if (!ps) return status;
     hipStream_t s_in = c.pstream[0], s_comp = c.pstream[1], s_out = c.pstream[2];
     ps->used_on(s_comp);

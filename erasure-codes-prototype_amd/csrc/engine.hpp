@@ -94,6 +94,7 @@ public:
                           int chunk_stripes);
 
     std::shared_ptr<ProgramSet> program_set(const std::vector<LinearOp>& progs, int* status);
+    std::shared_ptr<ProgramSet> program_set(const LinearOp* progs, size_t nprogs, int* status);
     int host_contexts() const;  // host-tier contexts created so far (pooled; bounded by concurrent calls)
     int device() const { return device_; }
     size_t cache_size();
@@ -102,7 +103,8 @@ public:
 
 private:
     explicit Engine(int device);
-    int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream);
+    // latency: the blocks are host memory read over PCIe (zero-copy host tier) -> GF_MODE_INLINE_LAT
+    int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream, bool latency = false);
 
     // Evicted sets wait here until nothing can read their tables: first until no caller holds them (no
     // further launch can be enqueued), then until a completion event recorded on every stream they were

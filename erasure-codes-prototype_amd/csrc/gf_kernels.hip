@@ -41,7 +41,7 @@ __device__ __forceinline__ const ECG_CONST T* cst(const T* p) {
 
 template <int MODE>
 __device__ __forceinline__ const uint8_t* src_ptr(const GfLaunch& a, int s, int prog, int j) {
-    if constexpr (MODE == GF_MODE_INLINE) {
+    if constexpr (MODE == GF_MODE_INLINE || MODE == GF_MODE_INLINE_LAT) {
         return a.isrc[j];
     } else if constexpr (MODE == GF_MODE_PTRS) {
         return cst(a.src_ptrs)[(size_t)s * a.k + j];
@@ -53,7 +53,7 @@ __device__ __forceinline__ const uint8_t* src_ptr(const GfLaunch& a, int s, int 
 
 template <int MODE>
 __device__ __forceinline__ uint8_t* dst_ptr(const GfLaunch& a, int s, int prog, int p) {
-    if constexpr (MODE == GF_MODE_INLINE) {
+    if constexpr (MODE == GF_MODE_INLINE || MODE == GF_MODE_INLINE_LAT) {
         return a.idst[p];
     } else if constexpr (MODE == GF_MODE_PTRS) {
         return cst(a.dst_ptrs)[(size_t)s * a.m + p];
@@ -189,7 +189,7 @@ __device__ __forceinline__ void wg_coords(const GfLaunch& a, int& s, int& w) {
 // Generic vector path: bytes [0, 16 * floor(B / 16)) of every block; all pointers 16-byte aligned.
 // grid.x = S * wg_per_stripe (stripe-major), grid.y = row tiles of MT outputs.
 template <int MT, int MODE, int NT, bool BIN>
-__global__ void __launch_bounds__(kThreads, occupancy_for(MT)) gf_vec_kernel(const GfLaunch a) {
+__global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occupancy_for(MT)) gf_vec_kernel(const GfLaunch a) {
     int s, w;
     wg_coords(a, s, w);
     const int rt = blockIdx.y;
@@ -215,6 +215,19 @@ __global__ void __launch_bounds__(kThreads, occupancy_for(MT)) gf_vec_kernel(con
             for (int d = 0; d < 4; ++d) acc[p][d] = 0u;
 
         int j = 0;
+        if constexpr (MODE == GF_MODE_INLINE_LAT) {
+            if (k <= 8) {  // uniform: every load in flight before the first use, then fold
+                // straight-line loads (a lane past k re-reads input 0): a branch per load would end the
+                // basic block and with it the overlap, one PCIe round trip per input
+                uint32_t x[8][4];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) load16<NT>(src_ptr<MODE>(a, s, prog, u < k ? u : 0) + off, x[u]);
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (u < k) fold<MT, 1, BIN>(reinterpret_cast<const uint32_t(&)[1][4]>(x[u]), T + (size_t)u * MT, acc);
+                j = k;
+            }
+        }
         for (; j + 4 <= k; j += 4) {
             uint32_t x[4][4];
 #pragma unroll
@@ -408,7 +421,8 @@ static bool outputs_in_stripe(const GfLaunch& a, int mode) {
 hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st) {
     if (base.k < 1 || base.m < 1 || base.S < 1 || base.B < 0 || base.MT < 1 || base.MT > kMaxMT)
         return hipErrorInvalidValue;
-    if (mode == GF_MODE_INLINE && (base.S != 1 || base.k > kInlineSrc || base.m > kInlineDst))
+    if ((mode == GF_MODE_INLINE || mode == GF_MODE_INLINE_LAT) &&
+        (base.S != 1 || base.k > kInlineSrc || base.m > kInlineDst))
         return hipErrorInvalidValue;
     if (base.B == 0) return hipSuccess;
     init_options();
@@ -432,6 +446,7 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         Launcher l = nullptr;
         switch (mode) {
             case GF_MODE_INLINE: l = pick_vec<GF_MODE_INLINE>(a, nt); break;
+            case GF_MODE_INLINE_LAT: l = pick_vec<GF_MODE_INLINE_LAT>(a, nt); break;
             case GF_MODE_PTRS: l = pick_vec<GF_MODE_PTRS>(a, nt); break;
             case GF_MODE_STRIDED: l = pick_vec<GF_MODE_STRIDED>(a, nt); break;
             default: return hipErrorInvalidValue;
@@ -453,7 +468,8 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         if (gx > 0x7fffffffLL) return hipErrorInvalidConfiguration;
         Launcher l = nullptr;
         switch (mode) {
-            case GF_MODE_INLINE: l = pick_byte<GF_MODE_INLINE>(a); break;
+            case GF_MODE_INLINE:
+            case GF_MODE_INLINE_LAT: l = pick_byte<GF_MODE_INLINE>(a); break;
             case GF_MODE_PTRS: l = pick_byte<GF_MODE_PTRS>(a); break;
             case GF_MODE_STRIDED: l = pick_byte<GF_MODE_STRIDED>(a); break;
             default: return hipErrorInvalidValue;

@@ -1,6 +1,8 @@
 // Host-side matrix construction and decode planning.  See matrix.hpp.
 #include "matrix.hpp"
 
+#include <unordered_map>
+
 #include <algorithm>
 
 #include <map>
@@ -351,6 +353,35 @@ int plan_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const in
     }
     ops.push_back(std::move(op));
     return 0;
+}
+
+std::shared_ptr<const std::vector<LinearOp>> encode_plan_cached(int k, int m, const int* matrix) {
+    struct Entry {
+        std::vector<int> key;
+        std::shared_ptr<const std::vector<LinearOp>> ops;
+    };
+    thread_local std::unordered_map<uint64_t, std::vector<Entry>> cache;
+    thread_local size_t entries = 0;
+    thread_local std::vector<int> key;
+    key.resize(2 + (size_t)k * m);
+    key[0] = k;
+    key[1] = m;
+    std::copy(matrix, matrix + (size_t)k * m, key.begin() + 2);
+    uint64_t h = 1469598103934665603ull;
+    for (int x : key) h = (h ^ (uint32_t)x) * 1099511628211ull;
+    auto& bucket = cache[h];
+    for (const Entry& e : bucket)
+        if (e.key == key) return e.ops;
+    if (++entries > 1024) {  // bounded: a long-running caller sees an open set of partial matrices
+        cache.clear();
+        entries = 1;
+    }
+    auto ops = std::make_shared<std::vector<LinearOp>>();
+    LinearOp op = plan_matrix_encode(k, m, matrix);
+    if (op.m_out() > 0) ops->push_back(std::move(op));
+    auto& b2 = cache[h];
+    b2.push_back(Entry{key, ops});
+    return b2.back().ops;
 }
 
 }  // namespace ecg

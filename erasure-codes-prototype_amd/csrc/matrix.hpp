@@ -3,6 +3,8 @@
 // (CmakeLists.txt:116-134); the region (byte) half is the HIP engine.
 #pragma once
 #include <stdint.h>
+
+#include <memory>
 #include <vector>
 
 namespace ecg {
@@ -54,5 +56,9 @@ int plan_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const in
 
 // An op is BINARY when every coefficient is 0 or 1 (pure XOR network).
 bool op_is_binary(const LinearOp& op);
+
+// plan_matrix_encode through a per-thread cache keyed by (k, m, matrix entries): the same plan object
+// for the same matrix, so per-stripe calls neither rebuild it nor copy it into a batch scope.
+std::shared_ptr<const std::vector<LinearOp>> encode_plan_cached(int k, int m, const int* matrix);
 
 }  // namespace ecg

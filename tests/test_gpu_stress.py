@@ -150,7 +150,15 @@ def test_eviction_does_not_stall_other_streams(ecg, oracle):
         M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
         big = torch.empty((S, k + m, B), dtype=torch.uint8, device="cuda")
         ecg.fill_random(big, 0xE71C)
+        rng = np.random.default_rng(7)
+        mine = torch.cuda.Stream()
+        Bs = 4096
+        blocks = torch.from_numpy(rng.integers(0, 256, (6, Bs), dtype=np.uint8)).cuda()
+        mats = [[int(x) for x in rng.integers(1, 256, 4 * 2)] for _ in range(24)]
+        outs = [torch.zeros((2, Bs), dtype=torch.uint8, device="cuda") for _ in mats]
         busy = torch.cuda.Stream()
+        # everything the evicting calls use is ready before the busy queue exists: a synchronize of the
+        # default stream after it would wait for the busy stream too (legacy default-stream semantics)
         torch.cuda.synchronize()
         ecg.encode_batch(k, m, M, big[:, :k], big[:, k:], stream=busy.cuda_stream)  # program built up front
         busy.synchronize()
@@ -161,13 +169,6 @@ def test_eviction_does_not_stall_other_streams(ecg, oracle):
         reps = max(20, int(0.4 / max(one, 1e-4)))  # ~0.4 s queued on `busy`
         for _ in range(reps):
             ecg.encode_batch(k, m, M, big[:, :k], big[:, k:], stream=busy.cuda_stream)
-        rng = np.random.default_rng(7)
-        mine = torch.cuda.Stream()
-        Bs = 4096
-        blocks = torch.from_numpy(rng.integers(0, 256, (6, Bs), dtype=np.uint8)).cuda()
-        mats = [[int(x) for x in rng.integers(1, 256, 4 * 2)] for _ in range(24)]
-        outs = [torch.zeros((2, Bs), dtype=torch.uint8, device="cuda") for _ in mats]
-        torch.cuda.current_stream().synchronize()  # inputs and zeroed outputs ready before `mine` runs
         t0 = time.time()
         for Mi, out in zip(mats, outs):  # every call a new program: evictions all along
             ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs,

@@ -1,0 +1,133 @@
+// Where the time of one small synchronous host-tier call goes (config 1's shape: RS(6,4), 1 KiB blocks,
+// one jerasure_matrix_encode per stripe on the proxy's host buffers, proxy.cpp:312-349).
+//   call     ecg_jerasure_matrix_encode, RS(6,4) 1 KiB (the product path: gather into pinned mapped
+//            staging, one zero-copy kernel over PCIe, synchronize, scatter back)
+//   empty    an empty kernel + hipStreamSynchronize on a non-blocking stream: the launch + completion
+//            round trip every synchronous GPU call pays, whatever it computes
+//   touch    a kernel that reads 6 KiB and writes 4 KiB of pinned mapped host memory (one 16-byte load per
+//            lane per block, like the product kernel) + synchronize: empty + the PCIe traffic
+//   par      the same with all six loads issued before the first use (one PCIe round trip)
+//   read1    one 1 KiB block read, four written;   write   four written, nothing read
+// Run under rocprofv3 --kernel-trace --hip-trace --stats to split each into API and kernel time.
+// Build: hipcc -O2 -std=c++20 --offload-arch=gfx950 -Iinclude tools/small_call.cpp -Lerasure-codes-prototype_amd/lib -lecg
+//        -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o tools/small_call
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "ecg.h"
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));    \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+__global__ void empty_kernel() {}
+
+// 64 lanes x 16 B = 1 KiB per block: each lane loads its 16 bytes of k input blocks and stores m outputs
+__global__ void touch_kernel(const uint4* in, uint4* out, int k, int m) {
+    const int lane = threadIdx.x;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < k; j++) {
+        const uint4 v = in[j * 64 + lane];
+        acc.x ^= v.x;
+        acc.y ^= v.y;
+        acc.z ^= v.z;
+        acc.w ^= v.w;
+    }
+    for (int p = 0; p < m; p++) out[p * 64 + lane] = acc;
+}
+
+// the same traffic with every load issued before the first use (compile-time K, M): one PCIe round trip
+template <int K, int M>
+__global__ void touch_parallel_kernel(const uint4* in, uint4* out) {
+    const int lane = threadIdx.x;
+    uint4 v[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) v[j] = in[j * 64 + lane];
+    uint4 acc = v[0];
+#pragma unroll
+    for (int j = 1; j < K; j++) {
+        acc.x ^= v[j].x;
+        acc.y ^= v[j].y;
+        acc.z ^= v[j].z;
+        acc.w ^= v[j].w;
+    }
+#pragma unroll
+    for (int p = 0; p < M; p++) out[p * 64 + lane] = acc;
+}
+
+// writes only (posted PCIe writes), no host reads
+__global__ void write_only_kernel(uint4* out, int m) {
+    const int lane = threadIdx.x;
+    for (int p = 0; p < m; p++) out[p * 64 + lane] = make_uint4(lane, p, 0, 0);
+}
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? atoi(argv[1]) : 4000;
+    const int k = 6, m = 4, B = 1024;
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    uint8_t *h = nullptr, *d = nullptr;
+    CK(hipHostMalloc((void**)&h, (size_t)(k + m) * B, hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipHostGetDevicePointer((void**)&d, h, 0));
+    for (int i = 0; i < (k + m) * B; i++) h[i] = (uint8_t)i;
+
+    int* M = ecg_reed_sol_vandermonde_coding_matrix(k, m, 8);
+    std::vector<char> value((size_t)k * B, 1);
+    std::vector<std::vector<char>> par(m, std::vector<char>(B, 0));
+    std::vector<char*> p(k + m);
+    for (int i = 0; i < k; i++) p[i] = value.data() + (size_t)i * B;
+    for (int i = 0; i < m; i++) p[k + i] = par[i].data();
+
+    auto bench = [&](const char* name, auto fn) {
+        for (int i = 0; i < 200; i++) fn();  // warm
+        double best = 1e9, sum = 0;
+        for (int r = 0; r < 5; r++) {
+            const double t0 = now();
+            for (int i = 0; i < N / 5; i++) fn();
+            const double us = (now() - t0) / (N / 5) * 1e6;
+            best = std::min(best, us);
+            sum += us;
+        }
+        printf("%-6s %7.2f us/call (best of 5 rounds), %7.2f avg\n", name, best, sum / 5);
+        fflush(stdout);
+    };
+    bench("call", [&] {
+        if (ecg_jerasure_matrix_encode(k, m, 8, M, p.data(), p.data() + k, B) != 0) exit(2);
+    });
+    bench("empty", [&] {
+        hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st);
+        CK(hipStreamSynchronize(st));
+    });
+    bench("touch", [&] {
+        hipLaunchKernelGGL(touch_kernel, dim3(1), dim3(64), 0, st, (const uint4*)d, (uint4*)(d + (size_t)k * B), k, m);
+        CK(hipStreamSynchronize(st));
+    });
+    bench("par", [&] {
+        hipLaunchKernelGGL((touch_parallel_kernel<6, 4>), dim3(1), dim3(64), 0, st, (const uint4*)d, (uint4*)(d + (size_t)k * B));
+        CK(hipStreamSynchronize(st));
+    });
+    bench("read1", [&] {
+        hipLaunchKernelGGL(touch_kernel, dim3(1), dim3(64), 0, st, (const uint4*)d, (uint4*)(d + (size_t)k * B), 1, m);
+        CK(hipStreamSynchronize(st));
+    });
+    bench("write", [&] {
+        hipLaunchKernelGGL(write_only_kernel, dim3(1), dim3(64), 0, st, (uint4*)(d + (size_t)k * B), m);
+        CK(hipStreamSynchronize(st));
+    });
+    ecg_free(M);
+    CK(hipHostFree(h));
+    return 0;
+}
