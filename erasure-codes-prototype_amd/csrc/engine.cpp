@@ -104,7 +104,33 @@ void set_last_error(const std::string& s) { t_last_error = s; }
 // Freed without waiting: a set that was ever launched is destroyed only by sweep_retired(), after its
 // launches completed; any other (a lost insertion race, a failed build) was never launched.
 ProgramSet::~ProgramSet() {
+    if (ready_ev) {
+        // a set dropped before its upload was seen complete (a lost insertion race): the copy must land
+        // before the memory is reused
+        if (!ready.load(std::memory_order_acquire)) (void)hipEventSynchronize(ready_ev);
+        (void)hipEventDestroy(ready_ev);
+    }
+    if (pinned) owner->release_pinned(pinned, pinned_class);
     if (mem) owner->release_tables(mem, mem_class);
+}
+
+// Before a launch on `st` reads the set's tables: once the upload event has fired the set is ready for
+// every stream; until then a launch on another stream than the uploading one waits for the event.
+int ProgramSet::ensure_ready(hipStream_t st) {
+    if (ready.load(std::memory_order_acquire)) return ECG_OK;
+    const hipError_t q = hipEventQuery(ready_ev);
+    if (q == hipSuccess) {
+        std::lock_guard<std::mutex> lk(smu);  // one thread hands the pinned source back
+        if (!ready.load(std::memory_order_relaxed)) {
+            if (pinned) owner->release_pinned(pinned, pinned_class);
+            pinned = nullptr;
+            ready.store(true, std::memory_order_release);
+        }
+        return ECG_OK;
+    }
+    if (q != hipErrorNotReady) return ECG_EHIP;
+    if (st != first_stream && hipStreamWaitEvent(st, ready_ev, 0) != hipSuccess) return ECG_EHIP;
+    return ECG_OK;
 }
 
 void* Engine::acquire_tables(size_t bytes, size_t* cls, hipError_t* err) {
@@ -125,6 +151,39 @@ void* Engine::acquire_tables(size_t bytes, size_t* cls, hipError_t* err) {
     void* p = nullptr;
     *err = hipMalloc(&p, c);
     return *err == hipSuccess ? p : nullptr;
+}
+
+void* Engine::acquire_pinned(size_t bytes, size_t* cls, hipError_t* err) {
+    size_t c = 256;
+    while (c < bytes) c <<= 1;
+    *cls = c;
+    *err = hipSuccess;
+    {
+        std::lock_guard<std::mutex> lk(pmu_);
+        auto it = pinned_pool_.find(c);
+        if (it != pinned_pool_.end() && !it->second.empty()) {
+            void* p = it->second.back();
+            it->second.pop_back();
+            pinned_pooled_bytes_ -= c;
+            return p;
+        }
+    }
+    void* p = nullptr;
+    *err = hipHostMalloc(&p, c, hipHostMallocDefault);
+    return *err == hipSuccess ? p : nullptr;
+}
+
+void Engine::release_pinned(void* p, size_t cls) {
+    constexpr size_t kPinnedCap = 16 << 20;
+    {
+        std::lock_guard<std::mutex> lk(pmu_);
+        if (pinned_pooled_bytes_ + cls <= kPinnedCap) {
+            pinned_pool_[cls].push_back(p);
+            pinned_pooled_bytes_ += cls;
+            return;
+        }
+    }
+    (void)hipHostFree(p);
 }
 
 void Engine::release_tables(void* p, size_t cls) {
@@ -211,11 +270,11 @@ size_t Engine::cache_size() {
     return cache_.size();
 }
 
-std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& progs, int* status) {
-    return program_set(progs.data(), progs.size(), status);
+std::shared_ptr<ProgramSet> Engine::program_set(const std::vector<LinearOp>& progs, int* status, hipStream_t st) {
+    return program_set(progs.data(), progs.size(), status, st);
 }
 
-std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t nprogs, int* status) {
+std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t nprogs, int* status, hipStream_t st) {
     *status = ECG_OK;
     if (nprogs == 0) {
         *status = ECG_EINVAL;
@@ -296,14 +355,25 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
     ps->d_tabs = (CoefTab*)ps->mem;
     ps->d_src = (int*)((uint8_t*)ps->mem + src_off);
     ps->d_dst = (int*)((uint8_t*)ps->mem + dst_off);
-    {
-        // a private non-blocking stream: the upload never waits for (or joins) other streams' work
-        std::lock_guard<std::mutex> lk(pmu_);
-        if (!upload_ && (e = hipStreamCreateWithFlags(&upload_, hipStreamNonBlocking)) != hipSuccess)
-            return fail(e, "hipStreamCreate(upload)");
-        if ((e = hipMemcpyAsync(ps->mem, host.data(), total, hipMemcpyHostToDevice, upload_)) != hipSuccess)
-            return fail(e, "hipMemcpyAsync(program tables)");
-        if ((e = hipStreamSynchronize(upload_)) != hipSuccess) return fail(e, "hipStreamSynchronize(upload)");
+    // The upload goes on the requesting stream, asynchronously, ahead of the launch that needs it: no
+    // host wait, and no other stream involved (streams share the runtime's few hardware queues, so a
+    // private upload stream could sit behind another thread's queued work).  Launches on other streams
+    // wait for `ready_ev` until it has fired (ensure_ready).  The host bytes stay with the set until then.
+    if ((e = hipEventCreateWithFlags(&ps->ready_ev, hipEventDisableTiming)) != hipSuccess)
+        return fail(e, "hipEventCreate(program tables)");
+    ps->pinned = acquire_pinned(total, &ps->pinned_class, &e);
+    if (!ps->pinned) return fail(e, "hipHostMalloc(program tables)");
+    memcpy(ps->pinned, host.data(), total);
+    ps->first_stream = st;
+    ps->used_on(st);
+    if ((e = hipMemcpyAsync(ps->mem, ps->pinned, total, hipMemcpyHostToDevice, st)) != hipSuccess) {
+        (void)hipStreamSynchronize(st);
+        return fail(e, "hipMemcpyAsync(program tables)");
+    }
+    if ((e = hipEventRecord(ps->ready_ev, st)) != hipSuccess) {
+        (void)hipStreamSynchronize(st);  // the copy may be in flight: the memory must not go back yet
+        ps->ready.store(true);
+        return fail(e, "hipEventRecord(program tables)");
     }
     std::vector<std::shared_ptr<ProgramSet>> evicted;  // retired outside the lock
     {
@@ -348,8 +418,9 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     }
     if (op.k_in() > kInlineSrc || op.m_out() > kInlineDst) return run_ptr_batch(op, {blocks}, B, st);
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set(&op, 1, &status);
+    std::shared_ptr<ProgramSet> ps = program_set(&op, 1, &status, st);
     if (!ps) return status;
+    if (const int rc = ps->ensure_ready(st); rc != ECG_OK) return rc;
     GfLaunch a;
     memset(&a, 0, sizeof(a));
     a.tabs = ps->d_tabs;
@@ -1294,8 +1365,9 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
     }
     if (progs.size() > 1 && !d_prog_of_stripe) return ECG_EINVAL;
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set(progs, &status);
+    std::shared_ptr<ProgramSet> ps = program_set(progs, &status, st);
     if (!ps) return status;
+    if (const int rc = ps->ensure_ready(st); rc != ECG_OK) return rc;
     GfLaunch a;
     memset(&a, 0, sizeof(a));
     a.tabs = ps->d_tabs;
@@ -1329,8 +1401,9 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
     if (S == 0 || B == 0) return ECG_OK;
     if (!d_src || !d_dst) return ECG_EINVAL;
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set(&prog, 1, &status);
+    std::shared_ptr<ProgramSet> ps = program_set(&prog, 1, &status, st);
     if (!ps) return status;
+    if (const int rc = ps->ensure_ready(st); rc != ECG_OK) return rc;
     GfLaunch a;
     memset(&a, 0, sizeof(a));
     a.tabs = ps->d_tabs;
@@ -1389,9 +1462,10 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     for (int j = 0; j < kin; j++) dev.src_ids[j] = j;
     for (int p = 0; p < mout; p++) dev.dst_ids[p] = p;
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set(&dev, 1, &status);
-    if (!ps) return status;
     hipStream_t s_in = c.pstream[0], s_comp = c.pstream[1], s_out = c.pstream[2];
+    std::shared_ptr<ProgramSet> ps = program_set(&dev, 1, &status, s_comp);
+    if (!ps) return status;
+    if (const int rc = ps->ensure_ready(s_comp); rc != ECG_OK) return rc;
     ps->used_on(s_comp);
     const uint8_t* hin = (const uint8_t*)h_in;
     uint8_t* hout = (uint8_t*)h_out;

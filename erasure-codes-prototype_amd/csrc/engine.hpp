@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -59,6 +60,13 @@ struct ProgramSet {
         if (nstreams < kMaxStreams) streams[nstreams++] = s;
         else overflow = true;
     }
+    // upload state (program_set): the tables are copied on the first requesting stream
+    hipEvent_t ready_ev = nullptr;
+    hipStream_t first_stream = nullptr;
+    std::atomic<bool> ready{false};
+    void* pinned = nullptr;  // source of the asynchronous upload (pinned pool block, returned once ready)
+    size_t pinned_class = 0;
+    int ensure_ready(hipStream_t st);
     ~ProgramSet();  // returns the memory at once: only reached when no launch can still read the tables
 };
 
@@ -93,8 +101,10 @@ public:
                           void* h_out, long long out_sstride, long long out_bstride, long long B, int S,
                           int chunk_stripes);
 
-    std::shared_ptr<ProgramSet> program_set(const std::vector<LinearOp>& progs, int* status);
-    std::shared_ptr<ProgramSet> program_set(const LinearOp* progs, size_t nprogs, int* status);
+    // The cached program set of `progs`, built (tables uploaded asynchronously on `st`) on a miss.  The
+    // caller launches on `st` after ps->ensure_ready(st).
+    std::shared_ptr<ProgramSet> program_set(const std::vector<LinearOp>& progs, int* status, hipStream_t st);
+    std::shared_ptr<ProgramSet> program_set(const LinearOp* progs, size_t nprogs, int* status, hipStream_t st);
     int host_contexts() const;  // host-tier contexts created so far (pooled; bounded by concurrent calls)
     int device() const { return device_; }
     size_t cache_size();
@@ -116,6 +126,10 @@ private:
     // hipFree synchronizes the device.  Uploads go through a private non-blocking stream.
     void* acquire_tables(size_t bytes, size_t* cls, hipError_t* err);
     void release_tables(void* p, size_t cls);
+    // the same for the pinned host blocks the uploads are copied from (a pageable source would make
+    // the asynchronous copy wait for the stream's earlier work)
+    void* acquire_pinned(size_t bytes, size_t* cls, hipError_t* err);
+    void release_pinned(void* p, size_t cls);
     friend struct ProgramSet;
 
     int device_;
@@ -134,9 +148,8 @@ private:
     std::mutex rmu_;
     std::vector<Retired> retired_;
     std::mutex pmu_;
-    std::unordered_map<size_t, std::vector<void*>> pool_;
-    size_t pooled_bytes_ = 0;
-    hipStream_t upload_ = nullptr;
+    std::unordered_map<size_t, std::vector<void*>> pool_, pinned_pool_;
+    size_t pooled_bytes_ = 0, pinned_pooled_bytes_ = 0;
 
 public:
     size_t retired_pending();  // evicted sets not yet freed (tests)

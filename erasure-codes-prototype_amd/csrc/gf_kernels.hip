@@ -216,14 +216,23 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
 
         int j = 0;
         if constexpr (MODE == GF_MODE_INLINE_LAT) {
-            if (k <= 8) {  // uniform: every load in flight before the first use, then fold
-                // straight-line loads (a lane past k re-reads input 0): a branch per load would end the
-                // basic block and with it the overlap, one PCIe round trip per input
+            // uniform: every load in flight before the first use, then fold.  Straight-line loads (a
+            // lane past k re-reads input 0): a branch per load would end the basic block and with it the
+            // overlap, one PCIe round trip per input.
+            if (k <= 8) {
                 uint32_t x[8][4];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) load16<NT>(src_ptr<MODE>(a, s, prog, u < k ? u : 0) + off, x[u]);
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
+                    if (u < k) fold<MT, 1, BIN>(reinterpret_cast<const uint32_t(&)[1][4]>(x[u]), T + (size_t)u * MT, acc);
+                j = k;
+            } else if (k <= 16) {
+                uint32_t x[16][4];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) load16<NT>(src_ptr<MODE>(a, s, prog, u < k ? u : 0) + off, x[u]);
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
                     if (u < k) fold<MT, 1, BIN>(reinterpret_cast<const uint32_t(&)[1][4]>(x[u]), T + (size_t)u * MT, acc);
                 j = k;
             }

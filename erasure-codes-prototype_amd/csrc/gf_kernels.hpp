@@ -30,7 +30,7 @@ enum GfMode : int {
     GF_MODE_PTRS = 1,     // device pointer tables src_ptrs[S][k], dst_ptrs[S][m]
     GF_MODE_STRIDED = 2,  // base + stripe/block strides + per-program block ids
     GF_MODE_INLINE_LAT = 3,  // INLINE for latency-bound calls on host memory read over PCIe (zero-copy
-                             // host tier): a lane issues all of its k <= 8 input loads before the first
+                             // host tier): a lane issues all of its k <= 16 input loads before the first
                              // use -- one PCIe round trip instead of one per group of loads
 };
 
