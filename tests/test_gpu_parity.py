@@ -254,6 +254,68 @@ def test_facade_partials_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
             assert same(da, db), ("dec", local, lsub, surv, lost)
 
 
+def test_config3_full_block_repairs(ecg, torch_cuda):
+    """BASELINE config 3 at its block size: Azure-LRC(12,2,2), 1 MiB blocks, single-block repair with
+    partial decoding for every local block (data and local parities), as the proxies issue it per stripe
+    (helper partial, main partial, perform_addition; handle_repair.cpp:249,371-376) -- once with the
+    partials in HBM and once composed away (batch_scratch).  Every repaired block must equal the lost one."""
+    torch = torch_cuda
+    S, B = 14, 1 << 20
+    ec, st, plan = _azure_repair_state(ecg, torch, S, B, 0xC3)
+    idx = torch.arange(S, device="cuda")
+    want = st[idx, torch.tensor([p[0] for p in plan], device="cuda")]
+    for scratch in (False, True):
+        partials = torch.full((S, 2, B), 0x77, dtype=torch.uint8, device="cuda")
+        out = torch.zeros((S, B), dtype=torch.uint8, device="cuda")
+        with ecg.batch() as scope:
+            if scratch:
+                scope.scratch(partials)
+            _repair_sequence(ec, st, plan, partials, out, B)
+        torch.cuda.synchronize()
+        assert torch.equal(out, want), scratch
+        assert bool((partials == 0x77).all()) == scratch
+
+
+def test_config4_full_block_merge(ecg, oracle, torch_cuda):
+    """BASELINE config 4 at its block size: two PC(4,1,4,1) stripes with 4 MiB blocks merged (x = 2,
+    horizontal) into PC(8,1,4,1).  Each data row's new row parity is two partial encodings of the
+    merged code (one per old stripe's half of the row, erasure_code.cpp:97-111 with the new stripe's block
+    ids, merge.cpp:82) plus perform_addition at the parity's proxy (handle_merge.cpp:159,319), on HBM
+    blocks in one batch scope with the partials as scratch.  Compared with the oracle's encoding of the
+    merged stripe."""
+    from oracle import ec_ref as E
+    torch = torch_cuda
+    B = 4 << 20
+    old = E.ec_factory(7, E.CodingParameters(k1=4, m1=1, k2=4, m2=1))
+    new_o = E.ec_factory(7, E.CodingParameters(k1=8, m1=1, k2=4, m2=1))
+    new_p = ecg.ec_factory(ecg.ECTYPE.PC, ecg.CodingParameters(k1=8, m1=1, k2=4, m2=1))
+    halves = [E.blocks(old.k, B, 40 + h) for h in range(2)]  # data of the two old stripes, row-major 4 x 4
+    # merged data in the new code's block-id order
+    data_new = [None] * new_o.k
+    for r in range(4):
+        for c in range(8):
+            data_new[new_o.rowcol2bid(r, c)] = halves[c // 4][old.rowcol2bid(r, c % 4)]
+    coding = E.zeros(new_o.m, B)
+    new_o.encode(data_new, coding, B)
+    stripe_new = data_new + coding
+    d_half = [torch.from_numpy(np.stack(h)).cuda() for h in halves]
+    partials = torch.full((4, 2, B), 0x5D, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((4, B), dtype=torch.uint8, device="cuda")
+    with ecg.batch() as scope:
+        scope.scratch(partials)
+        for r in range(4):
+            par = [new_o.rowcol2bid(r, 8)]
+            for h in range(2):
+                ids = [new_o.rowcol2bid(r, 4 * h + c) for c in range(4)]
+                blocks = [d_half[h][old.rowcol2bid(r, c)] for c in range(4)]
+                assert new_p.encode_partial_blocks_for_encoding(blocks, [partials[r, h]], B, ids, par) == 0
+            assert new_p.perform_addition([partials[r, 0], partials[r, 1]], [out[r]], B, 2, 1) == 0
+    torch.cuda.synchronize()
+    assert bool((partials == 0x5D).all())
+    for r in range(4):
+        assert np.array_equal(out[r].cpu().numpy(), stripe_new[new_o.rowcol2bid(r, 8)]), r
+
+
 def test_partial_plan_cache_tells_objects_apart(ecg, oracle, torch_cuda):
     """The per-thread plan cache of the partial calls is keyed by each object's state (class, parameters,
     sub-codes): objects of one class that differ only in a parameter the matrices depend on -- ERS
