@@ -254,3 +254,21 @@ def test_programs_packing_and_shape_checks(ecg):
         ecg.Programs([])
     with pytest.raises(ecg.EcgError):
         ecg.Programs([([[1, 2]], [0, 1], [5]), ([[1, 2, 3]], [0, 1, 2], [5])])
+
+
+def test_region_xor_on_coefficient_rows_needs_no_gpu(ecg):
+    """galois_region_xor on the reference's own operands -- int coefficient rows of the Cauchy-LRC
+    matrix builders, 4 * k bytes (lrc.cpp:1511,2140) -- is host matrix construction: it runs in place
+    with no GPU round trip (this container has no GPU, so a launch would fail with ECG_EHIP)."""
+    import ctypes
+
+    import numpy as np
+    rng = np.random.default_rng(5)
+    for k in (1, 6, 12, 24, 1024):  # up to 4096 bytes
+        a = rng.integers(0, 256, k, dtype=np.int32)  # k ints = 4 * k bytes
+        b = rng.integers(0, 256, k, dtype=np.int32)
+        want = a ^ b
+        rc = ecg.lib().ecg_galois_region_xor(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p),
+                                             a.nbytes)
+        assert rc == 0
+        assert np.array_equal(b, want)
