@@ -99,6 +99,33 @@ int main() {
         for (int i = 0; i < m; i++) CK(hipMemcpyAsync(sep[i].data(), d + (k + i) * B, B, hipMemcpyDeviceToHost, st));
         CK(hipStreamSynchronize(st));
     });
+    hipStream_t ds[4];
+    for (auto& x : ds) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    hipEvent_t kd;
+    CK(hipEventCreateWithFlags(&kd, hipEventDisableTiming));
+    for (int ns : {2, 4}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "(h) one H2D + per-block D2H on %d streams (separate)", ns);
+        bench(nm, [&] {
+            CK(hipMemcpyAsync(d, value.data(), k * B, hipMemcpyHostToDevice, st));
+            CK(hipEventRecord(kd, st));
+            for (int i = 0; i < ns; i++) CK(hipStreamWaitEvent(ds[i], kd, 0));
+            for (int i = 0; i < m; i++)
+                CK(hipMemcpyAsync(sep[i].data(), d + (k + i) * B, B, hipMemcpyDeviceToHost, ds[i % ns]));
+            for (int i = 0; i < ns; i++) CK(hipStreamSynchronize(ds[i]));
+        });
+    }
+    bench("(i) per-block D2H alone, 1 stream (separate)", [&] {
+        for (int i = 0; i < m; i++) CK(hipMemcpyAsync(sep[i].data(), d + (k + i) * B, B, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+    });
+    bench("(i') one D2H of 4 MiB alone (contiguous)", [&] {
+        CK(hipMemcpyAsync(coding.data(), d + k * B, m * B, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+    });
+    bench("(i'') per-block D2H alone, hipMemcpy (sync) each", [&] {
+        for (int i = 0; i < m; i++) CK(hipMemcpy(sep[i].data(), d + (k + i) * B, B, hipMemcpyDeviceToHost));
+    });
     bench("(b) hipHostRegister + DMA + unregister", [&] {
         CK(hipHostRegister(value.data(), k * B, hipHostRegisterDefault));
         CK(hipHostRegister(coding.data(), m * B, hipHostRegisterDefault));
