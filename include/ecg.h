@@ -138,15 +138,17 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
 int ecg_batch_begin(void);
 int ecg_batch_flush(void);
 int ecg_batch_end(void);
-/* Declare the device range [ptr, ptr + bytes) SCRATCH for the rest of the calling thread's scope
- * (ECG_EINVAL outside one).  A recorded call that writes a block inside scratch memory does not write
- * it: the flush keeps the linear combination the block would hold, and later recorded calls that read
- * the block read that combination's blocks instead.  So a partial result that only feeds a later call
+/* Declare the device range [ptr, ptr + bytes) SCRATCH in the calling thread's scope (ECG_EINVAL outside
+ * one).  The declaration holds until the scope ends and applies to every recorded call not yet flushed,
+ * whether recorded before or after it.  A recorded call that writes a block inside scratch memory does
+ * not write it: the flush keeps the linear combination the block would hold, and later recorded calls
+ * that read the block read that combination's blocks instead.  So a partial result that only feeds a later call
  * of the scope -- a helper or main proxy's partial decode (erasure_code.cpp:113-150) consumed by
  * perform_addition (erasure_code.cpp:70-94) on the same GPU, handle_repair.cpp:249,371-376 -- costs no
  * HBM write and re-read.  The combination is written for real when it must be: before a block it reads
- * is overwritten, when it is read on another stream, device or block size, and at a mid-scope flush.
- * After ecg_batch_end() the contents of scratch memory are undefined. */
+ * is overwritten, when it is read on another stream, device or block size, and at a mid-scope flush
+ * (ecg_batch_flush(), a host-tier or batched call inside the scope, or the automatic flush every 65536
+ * recorded calls).  After ecg_batch_end() the contents of scratch memory are undefined. */
 int ecg_batch_scratch(const void* ptr, size_t bytes);
 /* What this thread's last flush did: calls recorded, calls after scratch composition, launches (groups
  * x ops), scratch combinations written for real.  Any pointer may be NULL. */
