@@ -148,10 +148,10 @@ int main(int argc, char** argv) {
     }
     // Concurrent host-tier callers (the proxy runs encode on detached threads, proxy.cpp:416-419):
     // T threads, each with its own buffers, issuing synchronous RS(6,4) / RS(10,4) calls.
-    for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 65536}}) {
+    for (auto [kk, mm, B] : {std::tuple<int, int, int>{6, 4, 1024}, {10, 4, 65536}, {10, 4, 1 << 20}}) {
         int* Mh = ecg_reed_sol_vandermonde_coding_matrix(kk, mm, 8);
         for (int T : {1, 2, 4, 8, 16}) {
-            const int calls = 2000;
+            const int calls = B >= (1 << 20) ? 100 : 2000;
             std::vector<std::thread> th;
             std::atomic<int> errors{0};
             const double t0 = now();
@@ -165,8 +165,9 @@ int main(int argc, char** argv) {
                 });
             for (auto& x : th) x.join();
             const double dt = now() - t0;
-            printf("host tier RS(%d,%d) B=%6d  %2d threads: %8.0f calls/s  (%.1f us/call/thread)%s\n", kk, mm, B, T,
-                   T * calls / dt, dt / calls * 1e6, errors ? "  ERRORS" : "");
+            printf("host tier RS(%d,%d) B=%7d  %2d threads: %8.0f calls/s  (%.1f us/call/thread, %.1f GB/s over PCIe)%s\n",
+                   kk, mm, B, T, T * calls / dt, dt / calls * 1e6, (double)T * calls * (kk + mm) * B / dt / 1e9,
+                   errors ? "  ERRORS" : "");
             fflush(stdout);
         }
         ecg_free(Mh);
