@@ -154,12 +154,14 @@ __device__ __forceinline__ void fold(const uint32_t (&x)[U][4], const ECG_CONST 
 
 // Minimum waves per EU the register allocator must allow (r01 sweep, tools/gpu_variants.sh): 8 for the
 // 1-2-output kernels (decode, repair, XOR: +2 % at 8 vs 6), 6 for 3-4 outputs (encode: 8 costs 1 %),
-// 4 above.  ECG_OCC_OVERRIDE is for tuning builds only.
+// 4 above -- except 5 outputs: under the 128-VGPR cap of 4 waves the allocator spilled 12 bytes per lane
+// in the GENERAL flavour, while a hint of 3 lets it settle at 82 VGPRs (5 waves) with no scratch.
+// ECG_OCC_OVERRIDE is for tuning builds only.
 constexpr int occupancy_for(int MT) {
 #ifdef ECG_OCC_OVERRIDE
     return MT <= 4 ? ECG_OCC_OVERRIDE : 4;
 #else
-    return MT <= 2 ? 8 : MT <= 4 ? 6 : 4;
+    return MT <= 2 ? 8 : MT <= 4 ? 6 : MT == 5 ? 3 : 4;
 #endif
 }
 
