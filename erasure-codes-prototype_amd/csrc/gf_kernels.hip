@@ -168,19 +168,21 @@ constexpr int occupancy_for(int MT) {
 // Workgroup -> (stripe, column chunk).  grid_map 0: linear (workgroup b takes chunk b).  grid_map 1:
 // XCD-contiguous -- the dispatcher deals workgroups round-robin over the 8 XCDs, so b % 8 names the
 // XCD group; each group is given a contiguous 1/8 of the chunk list (T1 in the HIP guide; here for
-// DRAM locality of the concurrently active chunks, not L2 reuse).  grid_map 2: launch stripe s runs on
-// XCD group s % 8, chunks of a stripe in order.  Speed only, never correctness.
+// DRAM locality of the concurrently active chunks, not L2 reuse).  grid_map 2: runs of G = map_group
+// adjacent launch stripes are dealt round-robin to the XCD groups (G = 1: stripe s on group s % 8), each
+// group takes its stripes and their chunks in order.  Speed only, never correctness.
 __device__ __forceinline__ void wg_coords(const GfLaunch& a, int& s, int& w) {
     long long b = blockIdx.x;
     if (a.grid_map == 1) {
         const long long G = (long long)gridDim.x;
         const long long per = G >> 3;  // G % 8 == 0 is checked by the host
         b = (b & 7) * per + (b >> 3);
-    } else if (a.grid_map == 2) {  // stripe s runs on XCD group s % 8 (S % 8 == 0 checked by the host)
-        const long long i = b >> 3;
-        const long long srow = i / a.wg_per_stripe;
-        s = (int)(srow * 8 + (b & 7));
-        w = (int)(i - srow * a.wg_per_stripe);
+    } else if (a.grid_map == 2) {  // runs of G stripes dealt to the XCD groups (S % (8 G) == 0 checked by the host)
+        const long long i = b >> 3;                  // the i-th workgroup dealt to this XCD group
+        const long long ls = i / a.wg_per_stripe;    // the group's ls-th stripe, chunks in order
+        const long long G = a.map_group;
+        s = (int)(((ls / G) * 8 + (b & 7)) * G + ls % G);
+        w = (int)(i - ls * a.wg_per_stripe);
         return;
     }
     s = (int)(b / a.wg_per_stripe);
@@ -333,6 +335,7 @@ void init_options() {
     g_opt[ECG_OPT_GRID_MAP].store(env("ECG_GRID_MAP", 3));
     g_opt[ECG_OPT_ZEROCOPY_BYTES].store(env("ECG_ZEROCOPY_BYTES", 1 << 20));  // r01 host_latency.py
     g_opt[ECG_OPT_PROGRAM_CACHE].store(env("ECG_PROGRAM_CACHE", 4096));
+    g_opt[ECG_OPT_MAP_GROUP].store(env("ECG_MAP_GROUP", 1));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -415,6 +418,7 @@ int set_option(int opt, long long value) {
     if (opt == ECG_OPT_GRID_MAP && (value < 0 || value > 3)) return -1;
     if (opt == ECG_OPT_ZEROCOPY_BYTES && value < 0) return -1;
     if (opt == ECG_OPT_PROGRAM_CACHE && value < 2) return -1;
+    if (opt == ECG_OPT_MAP_GROUP && (value < 1 || value > (1 << 20))) return -1;
     g_opt[opt].store(value);
     return 0;
 }
@@ -451,8 +455,11 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         if (gx > 0x7fffffffLL) return hipErrorInvalidConfiguration;
         long long gm = g_opt[ECG_OPT_GRID_MAP].load();
         if (gm == 3) gm = outputs_in_stripe(a, mode) ? 1 : 2;
-        if (gm == 2 && a.S % 8 != 0) gm = 1;
+        long long G = g_opt[ECG_OPT_MAP_GROUP].load();
+        while (G > 1 && a.S % (8 * G) != 0) G >>= 1;  // the largest power-of-two divisor run that tiles S
+        if (gm == 2 && a.S % (8 * G) != 0) gm = 1;
         a.grid_map = (gm == 1 && gx % 8 == 0) ? 1 : (gm == 2) ? 2 : 0;
+        a.map_group = (int)G;
         const int nt = (int)g_opt[ECG_OPT_NT].load();
         Launcher l = nullptr;
         switch (mode) {

@@ -64,7 +64,8 @@ struct GfLaunch {
     int k, m, S;
     int MT, rtiles;
     int binary;          // every coefficient is 0 or 1 -> BINARY kernel flavour
-    int grid_map;        // 0 linear, 1 XCD-contiguous workgroup -> chunk mapping
+    int grid_map;        // 0 linear, 1 XCD-contiguous workgroup -> chunk mapping, 2 stripe groups per XCD
+    int map_group;       // grid_map 2: G adjacent stripes per XCD group (S % (8 G) == 0)
     int wg_per_stripe;
     int cols_per_wg;     // 16-byte columns per workgroup (vector path) / bytes per workgroup (byte path)
 };

@@ -37,7 +37,8 @@ ECG_OPT_COLS_PER_WG = 1
 ECG_OPT_GRID_MAP = 2
 ECG_OPT_ZEROCOPY_BYTES = 3
 ECG_OPT_PROGRAM_CACHE = 4
-ECG_OPT_COUNT = 5
+ECG_OPT_MAP_GROUP = 5
+ECG_OPT_COUNT = 6
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 

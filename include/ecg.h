@@ -52,7 +52,7 @@ int ecg_program_sets_retiring(void);
 int ecg_host_contexts(void);
 
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
- * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP).  Results never depend on them. */
+ * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP, ECG_MAP_GROUP).  Results never depend on them. */
 #define ECG_OPT_NT 0           /* non-temporal policy: bit 0 = loads, bit 1 = stores (default 3) */
 #define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 128; 0 = auto (128 = 2 KiB) */
 #define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous, 2 = stripe s on XCD group s%8,
@@ -63,7 +63,9 @@ int ecg_host_contexts(void);
 #define ECG_OPT_PROGRAM_CACHE 4 /* coefficient-table programs kept in HBM per device (LRU); when full, all
                                    but the newest half are dropped (freed after a device synchronize).
                                    Default 4096 */
-#define ECG_OPT_COUNT 5
+#define ECG_OPT_MAP_GROUP 5    /* grid map 2: adjacent stripes per XCD group run (default 1 = stripe s on
+                                  group s % 8); reduced to a power-of-two divisor tiling S when needed */
+#define ECG_OPT_COUNT 6
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

@@ -204,6 +204,9 @@ def test_tuning_options_validation(ecg):
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_COLS_PER_WG, 100) != 0  # not a multiple of the WG size
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_GRID_MAP, 4) != 0
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_PROGRAM_CACHE, 1) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_MAP_GROUP, 0) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_MAP_GROUP, 64) == 0
+        assert ecg.get_option(ecg.ECG_OPT_MAP_GROUP) == 64
         assert ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE) == saved[ecg.ECG_OPT_PROGRAM_CACHE]
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_COLS_PER_WG, 512) == 0
         assert ecg.get_option(ecg.ECG_OPT_COLS_PER_WG) == 512
@@ -212,6 +215,8 @@ def test_tuning_options_validation(ecg):
             ecg.set_option(o, v)
     if "ECG_GRID_MAP" not in os.environ:
         assert saved[ecg.ECG_OPT_GRID_MAP] == 3  # auto
+    if "ECG_MAP_GROUP" not in os.environ:
+        assert saved[ecg.ECG_OPT_MAP_GROUP] == 1
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])

@@ -846,21 +846,24 @@ def test_host_tier_staging_paths(ecg, oracle, torch_cuda, zc):
 
 
 def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
-    """Every ECG_OPT_* setting (grid map incl. auto, NT policy, chunk size) gives identical bytes, for an
-    in-stripe encode, a separate-buffer decode and S values that do / do not divide by 8."""
+    """Every ECG_OPT_* setting (grid map incl. auto, map-2 stripe groups, NT policy, chunk size) gives
+    identical bytes, for an in-stripe encode, a separate-buffer decode and S values that do / do not
+    divide by 8 (and by 8 G: G = 3 falls back to 1, G = 4 runs as is at S = 32)."""
     torch = torch_cuda
     k, m, B = 10, 4, 3 * 8192 + 16
     n = k + m
     M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
     saved = [ecg.get_option(o) for o in range(ecg.ECG_OPT_COUNT)]
     try:
-        for S in (16, 13):
+        for S in (32, 13):
             stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
             ecg.fill_random(stripes, 21 + S)
             ref_par, ref_dec = None, None
             pos = (torch.arange(S, device="cuda", dtype=torch.int32) % n).contiguous()
-            for gmap, nt, cpw in itertools.product((0, 1, 2, 3), (0, 3), (0, 256)):
+            maps = ((0, 1), (1, 1), (2, 1), (2, 2), (2, 3), (2, 4), (3, 1))
+            for (gmap, grp), nt, cpw in itertools.product(maps, (0, 3), (0, 256)):
                 ecg.set_option(ecg.ECG_OPT_GRID_MAP, gmap)
+                ecg.set_option(ecg.ECG_OPT_MAP_GROUP, grp)
                 ecg.set_option(ecg.ECG_OPT_NT, nt)
                 ecg.set_option(ecg.ECG_OPT_COLS_PER_WG, cpw)
                 stripes[:, k:].fill_(0xA5)
@@ -877,8 +880,8 @@ def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
                         assert same([h[s, k + i] for i in range(m)], par)
                     for s in range(S):
                         assert torch.equal(out[s, 0], stripes[s, s % n])
-                assert torch.equal(stripes[:, k:], ref_par), (S, gmap, nt, cpw)
-                assert torch.equal(out, ref_dec), (S, gmap, nt, cpw)
+                assert torch.equal(stripes[:, k:], ref_par), (S, gmap, grp, nt, cpw)
+                assert torch.equal(out, ref_dec), (S, gmap, grp, nt, cpw)
     finally:
         for o, v in enumerate(saved):
             ecg.set_option(o, v)
