@@ -186,11 +186,41 @@ def cpu_baseline(k, m, B, target_s):
         t_total += (t1 - t0) + (t3 - t2)
         reps += 1
     gib = reps * S * 2 * k * B / 2 ** 30
-    return {"value": round(gib / t_total, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+    line = {"value": round(gib / t_total, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "threads_used": threads, "cores_available": threads,
             "per_thread_GiBps": round(gib / t_total / threads, 3), **facts,
             "sample": f"{reps} x (encode + 1-erasure decode) of {S} RS({k},{m}) stripes x {B} B, "
                       f"one jerasure call per stripe, {threads} host threads, {t_total:.1f} s"}
+    aff = facts["affinity_cpus"]
+    if aff > threads:
+        # the quota caps CPU time, not threads: one thread per CPU of the affinity mask, shown to gain nothing
+        S2 = aff
+        data2 = np.ascontiguousarray(np.resize(data, (S2, k, B)))
+        stripes2 = np.zeros((S2, n, B), np.uint8)
+        stripes2[:, :k] = data2
+        coding2 = np.zeros((S2, m, B), np.uint8)
+        out2 = np.zeros((S2, B), np.uint8)
+        reps2, t2 = 0, 0.0
+        while t2 < target_s / 3 and reps2 < 100:
+            t0 = time.perf_counter()
+            ref.encode_batch_mt(k, m, M, data2, coding2, B, S2, aff)
+            t1 = time.perf_counter()
+            stripes2[:, k:] = coding2
+            t_mid = time.perf_counter()
+            ref.decode_batch_mt(k, m, M, stripes2, out2, B, S2, aff)
+            t2 += (t1 - t0) + (time.perf_counter() - t_mid)
+            reps2 += 1
+        check = {"threads": aff, "value": round(reps2 * S2 * 2 * k * B / 2 ** 30 / t2, 3), "unit": "GiB/s",
+                 "sample": f"{reps2} x (encode + 1-erasure decode) of {S2} stripes, one thread per CPU of the "
+                           f"affinity mask, {t2:.1f} s"}
+        if check["value"] > line["value"]:  # report whichever thread count the host actually rewards
+            quota_run = {key: line[key] for key in ("value", "sample")} | {"threads": threads, "unit": "GiB/s"}
+            line.update(value=check["value"], cores=aff, threads_used=aff, cores_available=aff,
+                        per_thread_GiBps=round(check["value"] / aff, 3), sample=check["sample"])
+            line["quota_threads_check"] = quota_run
+        else:
+            line["affinity_threads_check"] = check
+    return line
 
 
 # ------------------------------------------------------------------------------- config 2 (default)
