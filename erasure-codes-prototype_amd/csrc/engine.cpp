@@ -5,9 +5,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <functional>
 #include <map>
 #include <numeric>
+#include <thread>
 #include <tuple>
 
 #include "gf256.hpp"
@@ -1423,6 +1425,16 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
     return ECG_OK;
 }
 
+// Page-locked (hipHostMalloc'd or registered) host memory, as opposed to ordinary pageable memory.
+static bool host_pinned(const void* p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
 int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long in_sstride, long long in_bstride,
                               void* h_out, long long out_sstride, long long out_bstride, long long B, int S,
                               int chunk) {
@@ -1469,20 +1481,90 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     ps->used_on(s_comp);
     const uint8_t* hin = (const uint8_t*)h_in;
     uint8_t* hout = (uint8_t*)h_out;
-    bool used[3] = {false, false, false};
-    for (int s0 = 0, it = 0; s0 < S; s0 += chunk, it++) {
-        const int n = std::min(chunk, S - s0);
-        const int slot = it % 3;
+    const bool in_pinned = host_pinned(h_in), out_pinned = host_pinned(h_out);
+    const int nchunks = (int)((S + (long long)chunk - 1) / chunk);
+    auto issue_out = [&](int it) -> int {  // D2H of chunk it, behind its kernel
+        const int s0 = it * chunk, n = std::min(chunk, S - s0), slot = it % 3;
+        uint8_t* dout = c.pslot + (size_t)slot * (slot_in + slot_out) + slot_in;
+        ECG_HIP(hipStreamWaitEvent(s_out, c.comp_done[slot], 0));
+        for (int p = 0; p < mout; p++)
+            ECG_HIP(hipMemcpy2DAsync(hout + (size_t)s0 * out_sstride + (size_t)prog.dst_ids[p] * out_bstride,
+                                     (size_t)out_sstride, dout + (size_t)p * pitch, (size_t)mout * pitch, (size_t)B,
+                                     (size_t)n, hipMemcpyDeviceToHost, s_out));
+        ECG_HIP(hipEventRecord(c.out_done[slot], s_out));
+        return ECG_OK;
+    };
+    // A copy to or from pageable memory (the proxy's own vectors) returns only once the runtime has moved
+    // the bytes, so issued from one thread the input and output copies of a pageable batch run one after
+    // the other: RS(10,4) 1 MiB encode 36 GiB/s of data, the H2D and D2H times added.  PCIe is full
+    // duplex: with either side pageable, a second host thread issues the output copies (50 GiB/s, the
+    // pinned rate; profiles/r02/pipeline/).  Copying pageable runs of consecutive blocks as 1-D copies,
+    // which the runtime pins per copy above 1 MiB, measured slower than these 2-D copies and was dropped.  Chunk it's copies
+    // wait (host side) for its kernel to be enqueued; the kernel that reuses a slot waits until the copies
+    // that drain it are enqueued, so every event wait refers to the intended record.
+    struct OutThread {
+        std::mutex mu;
+        std::condition_variable cv;
+        int comp_issued = 0, out_issued = 0, rc = ECG_OK;
+        bool stop = false;
+        std::thread th;
+        void finish() {
+            if (!th.joinable()) return;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            th.join();
+        }
+        ~OutThread() { finish(); }
+    } ot;
+    const bool split = !in_pinned || !out_pinned;
+    if (split) {
+        ot.th = std::thread([&] {
+            if (hipSetDevice(device_) != hipSuccess) {  // the current device is per host thread
+                std::lock_guard<std::mutex> lk(ot.mu);
+                ot.rc = ECG_EHIP;
+                ot.cv.notify_all();
+                return;
+            }
+            for (int it = 0; it < nchunks; it++) {
+                {
+                    std::unique_lock<std::mutex> lk(ot.mu);
+                    ot.cv.wait(lk, [&] { return ot.comp_issued > it || ot.stop; });
+                    if (ot.comp_issued <= it) return;  // stopped early (error on the issuing thread)
+                }
+                const int rc = issue_out(it);
+                {
+                    std::lock_guard<std::mutex> lk(ot.mu);
+                    if (rc != ECG_OK) ot.rc = rc;
+                    else ot.out_issued = it + 1;
+                }
+                ot.cv.notify_all();
+                if (rc != ECG_OK) return;
+            }
+        });
+    }
+    for (int it = 0; it < nchunks; it++) {
+        const int s0 = it * chunk, n = std::min(chunk, S - s0), slot = it % 3;
+        const bool reuse = it >= 3;
         uint8_t* din = c.pslot + (size_t)slot * (slot_in + slot_out);
         uint8_t* dout = din + slot_in;
-        if (used[slot]) ECG_HIP(hipStreamWaitEvent(s_in, c.comp_done[slot], 0));  // slot's inputs consumed
+        if (reuse) ECG_HIP(hipStreamWaitEvent(s_in, c.comp_done[slot], 0));  // slot's inputs consumed
         for (int j = 0; j < kin; j++)
             ECG_HIP(hipMemcpy2DAsync(din + (size_t)j * pitch, (size_t)kin * pitch,
                                      hin + (size_t)s0 * in_sstride + (size_t)prog.src_ids[j] * in_bstride,
                                      (size_t)in_sstride, (size_t)B, (size_t)n, hipMemcpyHostToDevice, s_in));
         ECG_HIP(hipEventRecord(c.in_done[slot], s_in));
         ECG_HIP(hipStreamWaitEvent(s_comp, c.in_done[slot], 0));
-        if (used[slot]) ECG_HIP(hipStreamWaitEvent(s_comp, c.out_done[slot], 0));  // slot's outputs copied out
+        if (reuse) {
+            if (split) {  // the copies draining this slot (chunk it - 3) must be enqueued first
+                std::unique_lock<std::mutex> lk(ot.mu);
+                ot.cv.wait(lk, [&] { return ot.out_issued >= it - 2 || ot.rc != ECG_OK; });
+                if (ot.rc != ECG_OK) return ot.rc;
+            }
+            ECG_HIP(hipStreamWaitEvent(s_comp, c.out_done[slot], 0));  // slot's outputs copied out
+        }
         GfLaunch a;
         memset(&a, 0, sizeof(a));
         a.tabs = ps->d_tabs;
@@ -1503,13 +1585,19 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
         a.binary = ps->binary ? 1 : 0;
         ECG_HIP(launch_gf(a, GF_MODE_STRIDED, true, s_comp));
         ECG_HIP(hipEventRecord(c.comp_done[slot], s_comp));
-        ECG_HIP(hipStreamWaitEvent(s_out, c.comp_done[slot], 0));
-        for (int p = 0; p < mout; p++)
-            ECG_HIP(hipMemcpy2DAsync(hout + (size_t)s0 * out_sstride + (size_t)prog.dst_ids[p] * out_bstride,
-                                     (size_t)out_sstride, dout + (size_t)p * pitch, (size_t)mout * pitch, (size_t)B,
-                                     (size_t)n, hipMemcpyDeviceToHost, s_out));
-        ECG_HIP(hipEventRecord(c.out_done[slot], s_out));
-        used[slot] = true;
+        if (split) {
+            {
+                std::lock_guard<std::mutex> lk(ot.mu);
+                ot.comp_issued = it + 1;
+            }
+            ot.cv.notify_all();
+        } else if (const int rc = issue_out(it); rc != ECG_OK) {
+            return rc;
+        }
+    }
+    if (split) {
+        ot.th.join();
+        if (ot.rc != ECG_OK) return ot.rc;
     }
     ECG_HIP(hipStreamSynchronize(s_out));
     return lease.done();

@@ -773,11 +773,12 @@ def test_matrix_apply_multi_with_stripe_subset(ecg, oracle, torch_cuda):
         assert np.array_equal(hout[s, 1], ref[0]) and np.array_equal(hout[s, 0], ref[1]), s
 
 
-@pytest.mark.parametrize("B,S", [(65536 + 48, 11), ((1 << 20) + 16, 9)])
+@pytest.mark.parametrize("B,S", [(65536 + 48, 11), ((1 << 20) + 16, 9), (65536, 13), (1 << 20, 7)])
 @pytest.mark.parametrize("pinned", [False, True])
 def test_host_pipeline_encode_decode(ecg, oracle, torch_cuda, pinned, B, S):
     """Host-resident batches, pinned and pageable, through the H2D -> kernel -> D2H pipeline (chunks not
-    dividing S; 64 KiB and 1 MiB blocks)."""
+    dividing S; 64 KiB and 1 MiB blocks, with and without padded device slots).  On pageable buffers a
+    second host thread issues the output copies (engine.cpp run_host_pipeline)."""
     torch = torch_cuda
     k, m = 10, 4
     n = k + m
