@@ -6,6 +6,7 @@
 //   (c) T host threads memcpy into pinned staging, one DMA each way.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -145,6 +146,45 @@ int main() {
             CK(hipStreamSynchronize(st));
             par_memcpy(coding.data(), pin + k * B, m * B, T);
         });
+    }
+    {
+        // (j) per-block D2H copies issued from m persistent host threads, one stream each (a pageable copy
+        // blocks its issuing thread, so one thread runs the staged copies one after the other)
+        std::atomic<int> gen{0}, done{0};
+        std::atomic<bool> quit{false};
+        hipEvent_t ready;
+        CK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        std::vector<std::thread> pool;
+        for (int i = 0; i < m; i++)
+            pool.emplace_back([&, i] {
+                CK(hipSetDevice(0));
+                int seen = 0;
+                while (true) {
+                    int g;
+                    while ((g = gen.load(std::memory_order_acquire)) == seen && !quit.load()) {}
+                    if (quit.load()) return;
+                    seen = g;
+                    CK(hipStreamWaitEvent(ds[i], ready, 0));
+                    CK(hipMemcpyAsync(sep[i].data(), d + (k + i) * B, B, hipMemcpyDeviceToHost, ds[i]));
+                    CK(hipStreamSynchronize(ds[i]));
+                    done.fetch_add(1, std::memory_order_acq_rel);
+                }
+            });
+        bench("(j) one H2D + per-block D2H from m host threads", [&] {
+            CK(hipMemcpyAsync(d, value.data(), k * B, hipMemcpyHostToDevice, st));
+            CK(hipEventRecord(ready, st));
+            done.store(0);
+            gen.fetch_add(1, std::memory_order_acq_rel);
+            while (done.load(std::memory_order_acquire) < m) {}
+        });
+        bench("(j') per-block D2H alone from m host threads", [&] {
+            CK(hipEventRecord(ready, st));
+            done.store(0);
+            gen.fetch_add(1, std::memory_order_acq_rel);
+            while (done.load(std::memory_order_acquire) < m) {}
+        });
+        quit.store(true);
+        for (auto& t : pool) t.join();
     }
     bench("pinned DMA only (lower bound)", [&] {
         CK(hipMemcpyAsync(d, pin, k * B, hipMemcpyHostToDevice, st));
