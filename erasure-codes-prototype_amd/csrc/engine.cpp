@@ -459,6 +459,13 @@ struct DeferScope {
 
 thread_local DeferScope t_defer;
 constexpr size_t kMaxDeferred = 1 << 16;  // calls recorded before an automatic flush
+// Without declared scratch, a flush of the calls recorded so far changes nothing but where groups are
+// cut, so the scope flushes every kEagerFlush calls: the GPU runs the first calls while the host records
+// the rest, instead of idling until the scope ends.  (With scratch, a flush would write pending scratch
+// contents for real; such scopes flush only at kMaxDeferred.)
+constexpr size_t kEagerFlush = 1024;
+
+size_t flush_at() { return t_defer.scratch.empty() ? kEagerFlush : kMaxDeferred; }
 
 bool same_ops(const std::vector<LinearOp>& a, const std::vector<LinearOp>& b) {
     if (a.size() != b.size()) return false;
@@ -1183,7 +1190,7 @@ int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks,
         if (!t_defer.q.empty() && same_ops(*t_defer.q.back().ops, ops)) shared = t_defer.q.back().ops;
         else shared = std::make_shared<const std::vector<LinearOp>>(ops);
         t_defer.q.push_back(DeferredCall{this, st, B, std::move(shared), std::vector<uint8_t*>(blocks, blocks + nblocks)});
-        return t_defer.q.size() >= kMaxDeferred ? batch_flush() : ECG_OK;
+        return t_defer.q.size() >= flush_at() ? batch_flush() : ECG_OK;
     }
     return launch_direct(ops, blocks, B, st);
 }
@@ -1195,7 +1202,7 @@ int Engine::run_device(const std::shared_ptr<const std::vector<LinearOp>>& ops, 
     if (t_defer.active) {  // recorded with the caller's (interned) plan: no copy
         if (ops->empty() || B == 0) return ECG_OK;
         t_defer.q.push_back(DeferredCall{this, st, B, ops, std::vector<uint8_t*>(blocks, blocks + nblocks)});
-        return t_defer.q.size() >= kMaxDeferred ? batch_flush() : ECG_OK;
+        return t_defer.q.size() >= flush_at() ? batch_flush() : ECG_OK;
     }
     return launch_direct(*ops, blocks, B, st);
 }

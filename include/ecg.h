@@ -136,7 +136,9 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
  * included) flush first.  A group launches on the device its calls were recorded on, whatever the
  * thread's device at flush time.  If a launch fails, the flush returns its error and the calls of that
  * group and of all later groups are discarded (the scope stays open, empty).  Scopes do not nest
- * (ECG_EINVAL). */
+ * (ECG_EINVAL).  While no scratch is declared (ecg_batch_scratch), the scope also flushes by itself
+ * every 1024 recorded calls, so the GPU runs the first calls while the host records the rest; with
+ * scratch declared, only every 65536 calls.  Declare scratch before recording the calls it is for. */
 int ecg_batch_begin(void);
 int ecg_batch_flush(void);
 int ecg_batch_end(void);
