@@ -24,6 +24,12 @@ c1 = D.combine(int(x, 16) for x in rs1["parity_checksums"])
 c2 = D.combine(int(x, 16) for x in rs2["parity_checksums"])
 print(f"rs-encode-decode: N=1 512 stripes {c1:016x}; N=2 x 256 {c2:016x}; n_gpus={rs2['n_gpus']}")
 ok &= c1 == c2 and rs2["n_gpus"] == 2 and len(rs2["parity_checksums"]) == 2
+spawn = f"{d}/rs_n2_selfspawn.log"
+if os.path.exists(spawn):  # bench.py --gpus 2 started its own ranks (torch.distributed.run child)
+    rs2s = line(spawn)
+    c2s = D.combine(int(x, 16) for x in rs2s["parity_checksums"])
+    print(f"rs-encode-decode self-spawned: N=2 x 256 {c2s:016x}; n_gpus={rs2s['n_gpus']}")
+    ok &= c2s == c1 and rs2s["n_gpus"] == 2
 print(f"rs4m-waves: N=1 {w1['parity_checksum']}; N=2 {w2['parity_checksum']}")
 ok &= w1["parity_checksum"] == w2["parity_checksum"]
 for f in ("lrc_n2", "pc_n2", "ring_n2"):
