@@ -14,7 +14,7 @@ rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log; [ $rc -eq 0 ] || exit 
 timeout -k 10 600 python tools/microbench.py --out gpurun_out/micro.json > gpurun_out/micro.log 2>&1
 rc=$?; echo "micro rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 40 --warmup 3 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1
 rc=$?; echo "rocprof trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/pmc_fetch" -o fetch --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/pmc_fetch.log" 2>&1
 rc=$?; echo "rocprof fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
