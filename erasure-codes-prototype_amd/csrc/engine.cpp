@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -55,7 +56,13 @@ struct HostCtx {
     uint8_t* pinned = nullptr;      // host view
     uint8_t* pinned_dev = nullptr;  // device view (mapped, fine-grained)
     size_t pinned_cap = 0;
+    // zero-copy calls: completion flags the kernels post and the host polls (mapped, fine-grained)
+    unsigned* flags = nullptr;
+    unsigned* flags_dev = nullptr;
+    unsigned seq = 0;
+    unsigned unreaped = 0;  // flagged calls since the stream was last queried
 };
+constexpr int kFlagSlots = 1024;
 
 std::mutex g_ctx_mu[kMaxDevices];
 // never destroyed (process lifetime, like the engines): no teardown-order hazard with late callers
@@ -412,7 +419,9 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
 // One op over block pointers (device addresses), any k_in / m_out.  Ops that fit the kernel arguments
 // carry their pointers inline; wider ones (k_in > 128 or m_out > 32) go through an uploaded pointer
 // table (run_ptr_batch with one call), still asynchronous.
-int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st, bool latency) {
+int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st, bool latency,
+                       unsigned* flags, unsigned seq, int* n_flags) {
+    if (n_flags) *n_flags = 0;
     if (op.m_out() == 0 || B == 0) return ECG_OK;
     if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
         for (int d : op.dst_ids) ECG_HIP(hipMemsetAsync(blocks[d], 0, (size_t)B, st));
@@ -441,7 +450,9 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     for (int j = 0; j < op.k_in(); j++) a.isrc[j] = blocks[op.src_ids[j]];
     for (int p = 0; p < op.m_out(); p++) a.idst[p] = blocks[op.dst_ids[p]];
     ps->used_on(st);
-    ECG_HIP(launch_gf(a, latency ? GF_MODE_INLINE_LAT : GF_MODE_INLINE, vec_ok, st));
+    a.done_flags = latency ? flags : nullptr;
+    a.done_seq = seq;
+    ECG_HIP(launch_gf(a, latency ? GF_MODE_INLINE_LAT : GF_MODE_INLINE, vec_ok, st, n_flags));
     return ECG_OK;
 }
 
@@ -1207,6 +1218,56 @@ int Engine::run_device(const std::shared_ptr<const std::vector<LinearOp>>& ops, 
     return launch_direct(*ops, blocks, B, st);
 }
 
+// The context's completion-flag page (zero-copy host calls), allocated on first use.
+static bool flags_ready(HostCtx& c) {
+    if (c.flags) return true;
+    if (hipHostMalloc((void**)&c.flags, kFlagSlots * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        c.flags = nullptr;
+        return false;
+    }
+    if (hipHostGetDevicePointer((void**)&c.flags_dev, c.flags, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(c.flags);
+        c.flags = nullptr;
+        return false;
+    }
+    memset(c.flags, 0, kFlagSlots * sizeof(unsigned));
+    return true;
+}
+
+// Poll flags[0, n) until each holds seq.  A flag that does not arrive within 100 ms hands over to the
+// stream (a fault is reported there; a slow launch just finishes).  Every 64 flagged calls the stream is
+// queried so that the runtime retires the completed launches it never waited for.
+static int wait_flags(HostCtx& c, int n, unsigned seq, hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n; i++) {
+        while (__atomic_load_n(&c.flags[i], __ATOMIC_ACQUIRE) != seq) {
+            __builtin_ia32_pause();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+                ECG_HIP(hipStreamSynchronize(st));
+                for (int j = i; j < n; j++)
+                    if (__atomic_load_n(&c.flags[j], __ATOMIC_ACQUIRE) != seq) {
+                        set_last_error("zero-copy call: a completion flag never arrived");
+                        return ECG_EHIP;
+                    }
+                c.unreaped = 0;
+                return ECG_OK;
+            }
+        }
+    }
+    if (++c.unreaped >= 64) {
+        c.unreaped = 0;
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipSuccess && e != hipErrorNotReady) {
+            set_last_error(std::string("hipStreamQuery: ") + hipGetErrorString(e));
+            return ECG_EHIP;
+        }
+    }
+    return ECG_OK;
+}
+
 // Host-buffer tier (the reference's per-stripe calls on host memory).  Device slots are assigned to the
 // blocks that must be uploaded first (read before any op writes them), then to the rest, so the
 // inputs form one contiguous range.  Small calls (the proxy's 1 KiB - 64 KiB blocks) gather those
@@ -1284,14 +1345,32 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
             dev[id] = c.pinned_dev + (size_t)slot[id] * pitch;
             if (upload[id]) memcpy(c.pinned + (size_t)slot[id] * pitch, blocks[id], (size_t)B);
         }
+        // Completion by flags: every workgroup posts a flag once its stores are visible to the host, and the
+        // host polls the flags instead of synchronizing the stream -- the runtime's completion round trip is
+        // ~4 us of a ~14 us call (tools/small_call.cpp, profiles/r02/small_call/).  Only for launches whose
+        // vector path covers every byte and that fit the flag page; anything else synchronizes as before.
+        bool flagged = (B % 16) == 0 && flags_ready(c);
+        for (const LinearOp& op : ops)
+            flagged &= op.k_in() > 0 && op.k_in() <= kInlineSrc && op.m_out() <= kInlineDst;
+        const unsigned seq = ++c.seq == 0 ? ++c.seq : c.seq;  // flags start at 0: never post 0
+        int nflags = 0;
         for (const LinearOp& op : ops) {
-            int rc = launch_one(op, dev.data(), B, st, /*latency=*/true);
+            const long long wg_max = ((B / 16 + kThreads - 1) / kThreads) * op.m_out();  // >= chunks x row tiles
+            const bool f = flagged && nflags + wg_max <= kFlagSlots;
+            flagged = f;
+            int posted = 0;
+            int rc = launch_one(op, dev.data(), B, st, /*latency=*/true, f ? c.flags_dev + nflags : nullptr, seq, &posted);
             if (rc != ECG_OK) {
                 (void)hipStreamSynchronize(st);
                 return rc;
             }
+            nflags += posted;
         }
-        ECG_HIP(hipStreamSynchronize(st));
+        if (flagged) {
+            if (const int rc = wait_flags(c, nflags, seq, st); rc != ECG_OK) return rc;
+        } else {
+            ECG_HIP(hipStreamSynchronize(st));
+        }
         for (int id = 0; id < nblocks; id++)
             if (written[id]) memcpy(blocks[id], c.pinned + (size_t)slot[id] * pitch, (size_t)B);
         return lease.done();

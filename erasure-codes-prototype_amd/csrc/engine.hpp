@@ -114,7 +114,10 @@ public:
 private:
     explicit Engine(int device);
     // latency: the blocks are host memory read over PCIe (zero-copy host tier) -> GF_MODE_INLINE_LAT
-    int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream, bool latency = false);
+    // latency: the zero-copy host-tier variant; with flags (device view), it also posts completion flags
+    // at flags[0, *n_flags) with value seq (GfLaunch::done_flags)
+    int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream, bool latency = false,
+                   unsigned* flags = nullptr, unsigned seq = 0, int* n_flags = nullptr);
 
     // Evicted sets wait here until nothing can read their tables: first until no caller holds them (no
     // further launch can be enqueued), then until a completion event recorded on every stream they were

@@ -263,6 +263,15 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
         for (int p = 0; p < MT; ++p)
             if (p < nrows) store16<NT>(dst[p] + off, acc[p]);
     }
+    if constexpr (MODE == GF_MODE_INLINE_LAT) {
+        if (a.done_flags) {  // completion flag for a polling host (vector stores only)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's stores reach the host
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(a.done_flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // Byte path: bytes [off0, B) (tails, unaligned pointers).  cols_per_wg = bytes per workgroup.
@@ -433,7 +442,8 @@ static bool outputs_in_stripe(const GfLaunch& a, int mode) {
     return a.out_sstride == a.in_sstride && o >= a.in_base && o < a.in_base + a.in_sstride;
 }
 
-hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st) {
+hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st, int* n_wg) {
+    if (n_wg) *n_wg = 0;
     if (base.k < 1 || base.m < 1 || base.S < 1 || base.B < 0 || base.MT < 1 || base.MT > kMaxMT)
         return hipErrorInvalidValue;
     if ((mode == GF_MODE_INLINE || mode == GF_MODE_INLINE_LAT) &&
@@ -470,10 +480,13 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
             default: return hipErrorInvalidValue;
         }
         if (!l) return hipErrorInvalidValue;
+        if (a.done_flags && (mode != GF_MODE_INLINE_LAT || vec_bytes < a.B)) return hipErrorInvalidValue;
         l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+        if (n_wg) *n_wg = (int)(gx * a.rtiles);
     }
+    if (a.done_flags && vec_bytes < a.B) return hipErrorInvalidValue;  // the byte kernel posts no flags
     if (vec_bytes < a.B) {
         const long long nbytes = a.B - vec_bytes;
         long long bpw = 16LL * kThreads;

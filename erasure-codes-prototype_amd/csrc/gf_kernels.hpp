@@ -68,6 +68,12 @@ struct GfLaunch {
     int map_group;       // grid_map 2: G adjacent stripes per XCD group (S % (8 G) == 0)
     int wg_per_stripe;
     int cols_per_wg;     // 16-byte columns per workgroup (vector path) / bytes per workgroup (byte path)
+    // GF_MODE_INLINE_LAT only: completion flags in mapped host memory.  When set, every workgroup writes
+    // done_seq into done_flags[blockIdx.y * gridDim.x + blockIdx.x] after its stores are visible to the
+    // host (system-scope release), so a synchronous host call can poll them instead of synchronizing
+    // the stream.  Needs the vector path to cover every byte (no tail launch).
+    unsigned* done_flags;
+    unsigned done_seq;
 };
 
 // Runtime tuning options (ecg_set_option): see ECG_OPT_* in include/ecg.h.
@@ -76,7 +82,7 @@ int set_option(int opt, long long value);
 
 // Launch the region product over bytes [0, B) of every stripe.  `vec_ok` = every block pointer is
 // 16-byte aligned (the host checks); otherwise the byte path covers everything.  Returns a hipError_t.
-hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t stream);
+hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t stream, int* n_wg = nullptr);
 
 // Deterministic synthetic bytes: 8-byte word w = splitmix64(seed + (word_offset + w) * golden).
 hipError_t launch_fill_splitmix(void* dst, long long nbytes, unsigned long long seed,

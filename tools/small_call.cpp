@@ -74,6 +74,44 @@ __global__ void write_only_kernel(uint4* out, int m) {
     for (int p = 0; p < m; p++) out[p * 64 + lane] = make_uint4(lane, p, 0, 0);
 }
 
+// completion flag in mapped host memory: after the wave's stores, lane 0 publishes `seq` with a
+// system-scope release (a vector store); the host spins on the flag instead of synchronizing the stream
+__device__ __forceinline__ void publish(unsigned* flag, unsigned seq) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void empty_flag_kernel(unsigned* flag, unsigned seq) { publish(flag, seq); }
+
+template <int K, int M>
+__global__ void touch_parallel_flag_kernel(const uint4* in, uint4* out, unsigned* flag, unsigned seq) {
+    const int lane = threadIdx.x;
+    uint4 v[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) v[j] = in[j * 64 + lane];
+    uint4 acc = v[0];
+#pragma unroll
+    for (int j = 1; j < K; j++) {
+        acc.x ^= v[j].x;
+        acc.y ^= v[j].y;
+        acc.z ^= v[j].z;
+        acc.w ^= v[j].w;
+    }
+#pragma unroll
+    for (int p = 0; p < M; p++) out[p * 64 + lane] = acc;
+    publish(flag, seq);
+}
+
+static void spin(volatile unsigned* flag, unsigned seq, hipStream_t st) {
+    const double t0 = now();
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+        if (now() - t0 > 1.0) {  // never wait forever on a flag: fall back to the stream
+            CK(hipStreamSynchronize(st));
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) { fprintf(stderr, "flag never set\n"); exit(3); }
+            return;
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 4000;
     const int k = 6, m = 4, B = 1024;
@@ -127,6 +165,32 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(write_only_kernel, dim3(1), dim3(64), 0, st, (uint4*)(d + (size_t)k * B), m);
         CK(hipStreamSynchronize(st));
     });
+    unsigned* hflag = nullptr;
+    unsigned* dflag = nullptr;
+    CK(hipHostMalloc((void**)&hflag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipHostGetDevicePointer((void**)&dflag, hflag, 0));
+    *hflag = 0;
+    unsigned seq = 0;
+    bench("emptyF", [&] {
+        ++seq;
+        hipLaunchKernelGGL(empty_flag_kernel, dim3(1), dim3(64), 0, st, dflag, seq);
+        spin(hflag, seq, st);
+    });
+    bench("parF", [&] {
+        ++seq;
+        hipLaunchKernelGGL((touch_parallel_flag_kernel<6, 4>), dim3(1), dim3(64), 0, st, (const uint4*)d,
+                           (uint4*)(d + (size_t)k * B), dflag, seq);
+        spin(hflag, seq, st);
+    });
+    bench("parF+s", [&] {  // the flag, then a stream synchronize that should find the kernel done
+        ++seq;
+        hipLaunchKernelGGL((touch_parallel_flag_kernel<6, 4>), dim3(1), dim3(64), 0, st, (const uint4*)d,
+                           (uint4*)(d + (size_t)k * B), dflag, seq);
+        spin(hflag, seq, st);
+        CK(hipStreamSynchronize(st));
+    });
+    CK(hipStreamSynchronize(st));
+    CK(hipHostFree(hflag));
     ecg_free(M);
     CK(hipHostFree(h));
     return 0;
