@@ -846,6 +846,32 @@ def test_host_tier_staging_paths(ecg, oracle, torch_cuda, zc):
         ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, saved)
 
 
+def test_zero_copy_completion_flags_back_to_back(ecg, oracle, torch_cuda):
+    """Zero-copy host calls complete by polled flags, never by a stream synchronize (engine.cpp
+    wait_flags): 1500 back-to-back calls on fresh data, each result read right after its flags, cycling
+    through flagged shapes (1 KiB, 64 KiB: 32 workgroups, a 2-op decode) and ones that synchronize
+    instead (B % 16 != 0: the byte kernel posts no flags), so a stale flag or an early read would show as
+    a wrong byte.  More than 64 flagged calls, so the periodic stream query runs too."""
+    k, m = 6, 4
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    rng = np.random.default_rng(0xF1A6)
+    for i in range(1500):
+        B = (1024, 1000, 65536, 1024, 4096 + 48)[i % 5]
+        data = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(k)]
+        got = [np.full(B, 0x5A, np.uint8) for _ in range(m)]
+        assert ecg.jerasure_matrix_encode(k, m, M, data, got, B) == 0
+        want = [np.zeros(B, np.uint8) for _ in range(m)]
+        oracle.jerasure_matrix_encode(k, m, M, data, want, B)
+        assert same(got, want), (i, B)
+        if i % 50 == 0:  # two erasures: one composed decode op per call
+            stripe = [x.copy() for x in data + want]
+            S = [x.copy() for x in stripe]
+            S[1][:] = 0
+            S[k + 2][:] = 0
+            assert ecg.jerasure_matrix_decode(k, m, M, 1, [1, k + 2, -1], S[:k], S[k:], B) == 0
+            assert same(S, stripe), (i, B)
+
+
 def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
     """Every ECG_OPT_* setting (grid map incl. auto, map-2 stripe groups, NT policy, chunk size) gives
     identical bytes, for an in-stripe encode, a separate-buffer decode and S values that do / do not
