@@ -62,7 +62,7 @@ struct HostCtx {
     unsigned seq = 0;
     unsigned unreaped = 0;  // flagged calls since the stream was last queried
 };
-constexpr int kFlagSlots = 1024;
+constexpr int kFlagSlots = 4096;
 
 std::mutex g_ctx_mu[kMaxDevices];
 // never destroyed (process lifetime, like the engines): no teardown-order hazard with late callers

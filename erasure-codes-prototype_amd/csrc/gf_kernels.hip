@@ -342,7 +342,9 @@ void init_options() {
     g_opt[ECG_OPT_NT].store(env("ECG_NT", 3));
     g_opt[ECG_OPT_COLS_PER_WG].store(env("ECG_COLS_PER_WG", 0));
     g_opt[ECG_OPT_GRID_MAP].store(env("ECG_GRID_MAP", 3));
-    g_opt[ECG_OPT_ZEROCOPY_BYTES].store(env("ECG_ZEROCOPY_BYTES", 1 << 20));  // r01 host_latency.py
+    // every staged call (r02 host_latency.py --sweep-zc: zero-copy with completion flags beats DMA staging
+    // at every block size up to kStagedMaxBlock)
+    g_opt[ECG_OPT_ZEROCOPY_BYTES].store(env("ECG_ZEROCOPY_BYTES", 8 << 20));
     g_opt[ECG_OPT_PROGRAM_CACHE].store(env("ECG_PROGRAM_CACHE", 4096));
     g_opt[ECG_OPT_MAP_GROUP].store(env("ECG_MAP_GROUP", 1));
     g_opt_init.store(1, std::memory_order_release);

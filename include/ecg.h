@@ -58,10 +58,12 @@ int ecg_host_contexts(void);
 #define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous, 2 = stripe s on XCD group s%8,
                                   3 = auto (default): 1 when outputs live inside the input stripes, else 2 */
 #define ECG_OPT_ZEROCOPY_BYTES 3 /* host-buffer calls whose staged blocks total at most this many bytes
-                                    run the kernel on mapped pinned memory (no DMA); 0 = never;
-                                    default 1 MiB */
+                                    run the kernel on mapped pinned memory (no DMA) and complete by
+                                    polled flags; 0 = never; default 8 MiB (every staged call: blocks of
+                                    at most 256 KiB) */
 #define ECG_OPT_PROGRAM_CACHE 4 /* coefficient-table programs kept in HBM per device (LRU); when full, all
-                                   but the newest half are dropped (freed after a device synchronize).
+                                   but the newest half are dropped (retired: freed once the launches that
+                                   used them completed, by per-stream events, never a device synchronize).
                                    Default 4096 */
 #define ECG_OPT_MAP_GROUP 5    /* grid map 2: adjacent stripes per XCD group run (default 1 = stripe s on
                                   group s % 8); reduced to a power-of-two divisor tiling S when needed */

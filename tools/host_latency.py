@@ -28,11 +28,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=2000)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--sweep-zc", action="store_true",
+                    help="zero-copy threshold sweep: RS(10,4) 32-256 KiB blocks, DMA staging vs zero-copy")
     a = ap.parse_args()
     rng = np.random.default_rng(0)
     res = {}
-    for zc, k, m, B in [(zc, k, m, B) for zc in (0, 1 << 20) for k, m, B in
-                        [(6, 4, 1024), (10, 4, 1024), (10, 4, 16384), (10, 4, 65536), (10, 4, 1 << 20)]]:
+    cases = [(zc, k, m, B) for zc in (0, 1 << 20) for k, m, B in
+             [(6, 4, 1024), (10, 4, 1024), (10, 4, 16384), (10, 4, 65536), (10, 4, 1 << 20)]]
+    if a.sweep_zc:
+        cases = [(zc, 10, 4, B) for B in (32768, 65536, 98304, 131072, 196608, 262144) for zc in (0, 1 << 26)]
+    for zc, k, m, B in cases:
         ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, zc)
         M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
         data = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(k)]
