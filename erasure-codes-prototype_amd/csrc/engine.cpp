@@ -1237,15 +1237,20 @@ static bool flags_ready(HostCtx& c) {
     return true;
 }
 
-// Poll flags[0, n) until each holds seq.  A flag that does not arrive within 100 ms hands over to the
+// Poll flags[0, n) until each holds seq (spinning for the first 200 us, then yielding the core between
+// polls).  A flag that does not arrive within 100 ms hands over to the
 // stream (a fault is reported there; a slow launch just finishes).  Every 64 flagged calls the stream is
 // queried so that the runtime retires the completed launches it never waited for.
 static int wait_flags(HostCtx& c, int n, unsigned seq, hipStream_t st) {
     const auto t0 = std::chrono::steady_clock::now();
     for (int i = 0; i < n; i++) {
         while (__atomic_load_n(&c.flags[i], __ATOMIC_ACQUIRE) != seq) {
-            __builtin_ia32_pause();
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+            const auto waited = std::chrono::steady_clock::now() - t0;
+            if (waited < std::chrono::microseconds(200))
+                __builtin_ia32_pause();
+            else
+                std::this_thread::yield();  // queued behind other work: stop burning the core
+            if (waited > std::chrono::milliseconds(100)) {
                 ECG_HIP(hipStreamSynchronize(st));
                 for (int j = i; j < n; j++)
                     if (__atomic_load_n(&c.flags[j], __ATOMIC_ACQUIRE) != seq) {
