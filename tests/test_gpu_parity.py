@@ -1052,6 +1052,41 @@ def test_batch_scope_per_stripe_calls(ecg, oracle, torch_cuda):
         assert all(np.array_equal(coding[i], host[s, k + i]) for i in range(m))
 
 
+@pytest.mark.parametrize("with_scratch", [False, True])
+def test_batch_scope_eager_flush(ecg, torch_cuda, with_scratch):
+    """Without declared scratch the scope flushes by itself every 1024 recorded calls (the GPU works while
+    the host records); with scratch it keeps recording up to 65536.  3000 calls -- an encode per stripe,
+    then a perform_addition per stripe reading that stripe's parities -- cross the 1024 boundaries with
+    dependences on both sides, and give the bytes of the same calls made outside any scope."""
+    torch = torch_cuda
+    k, m, S, B = 4, 2, 1500, 256 + 16
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    st = torch.empty((S, k + m, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, 0xEA6E)
+    st[:, k:] = 0x5A
+    out = torch.zeros((S, B), dtype=torch.uint8, device="cuda")
+    ref_st, ref_out = st.clone(), out.clone()
+    dummy = torch.empty(4096, dtype=torch.uint8, device="cuda")
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
+
+    def calls(x, o):
+        for s in range(S):
+            ec.encode([x[s, j] for j in range(k)], [x[s, k + i] for i in range(m)], B)
+        for s in range(S):
+            ec.perform_addition([x[s, k], x[s, k + 1]], [o[s]], B, 2, 1)
+
+    calls(ref_st, ref_out)
+    with ecg.batch() as scope:
+        if with_scratch:
+            scope.scratch(dummy)  # unrelated scratch: nothing composes, but no eager flush either
+        calls(st, out)
+    torch.cuda.synchronize()
+    assert torch.equal(st, ref_st) and torch.equal(out, ref_out)
+    assert bool((out == (st[:, k] ^ st[:, k + 1])).all())
+    stats = ecg.batch_last_stats()
+    assert stats["recorded"] == (2 * S if with_scratch else (2 * S) % 1024), stats
+
+
 def test_batch_scope_hazards_split_runs(ecg, torch_cuda):
     """Calls with the same plan that depend on each other (a chain of galois_region_xor-like additions
     through perform_addition) must keep their sequential meaning inside a scope."""
