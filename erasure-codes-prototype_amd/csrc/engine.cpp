@@ -1590,13 +1590,14 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     // the other: RS(10,4) 1 MiB encode 36 GiB/s of data, the H2D and D2H times added.  PCIe is full
     // duplex: with either side pageable, a second host thread issues the output copies (50 GiB/s, the
     // pinned rate; profiles/r02/pipeline/).  Copying pageable runs of consecutive blocks as 1-D copies,
-    // which the runtime pins per copy above 1 MiB, measured slower than these 2-D copies and was dropped.  Chunk it's copies
-    // wait (host side) for its kernel to be enqueued; the kernel that reuses a slot waits until the copies
-    // that drain it are enqueued, so every event wait refers to the intended record.
+    // which the runtime pins per copy above 1 MiB, measured slower than these 2-D copies and was dropped.
+    // Chunk it's copies wait (host side) for its kernel to be enqueued; the kernel that reuses a slot waits
+    // until the copies that drain it are enqueued, so every event wait refers to the intended record.
     struct OutThread {
         std::mutex mu;
         std::condition_variable cv;
         int comp_issued = 0, out_issued = 0, rc = ECG_OK;
+        std::string msg;  // the copy thread's error message (last_error is per thread)
         bool stop = false;
         std::thread th;
         void finish() {
@@ -1616,6 +1617,7 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
             if (hipSetDevice(device_) != hipSuccess) {  // the current device is per host thread
                 std::lock_guard<std::mutex> lk(ot.mu);
                 ot.rc = ECG_EHIP;
+                ot.msg = "host pipeline: hipSetDevice failed on the copy thread";
                 ot.cv.notify_all();
                 return;
             }
@@ -1628,8 +1630,12 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
                 const int rc = issue_out(it);
                 {
                     std::lock_guard<std::mutex> lk(ot.mu);
-                    if (rc != ECG_OK) ot.rc = rc;
-                    else ot.out_issued = it + 1;
+                    if (rc != ECG_OK) {
+                        ot.rc = rc;
+                        ot.msg = last_error_string();
+                    } else {
+                        ot.out_issued = it + 1;
+                    }
                 }
                 ot.cv.notify_all();
                 if (rc != ECG_OK) return;
@@ -1652,7 +1658,10 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
             if (split) {  // the copies draining this slot (chunk it - 3) must be enqueued first
                 std::unique_lock<std::mutex> lk(ot.mu);
                 ot.cv.wait(lk, [&] { return ot.out_issued >= it - 2 || ot.rc != ECG_OK; });
-                if (ot.rc != ECG_OK) return ot.rc;
+                if (ot.rc != ECG_OK) {
+                    set_last_error(ot.msg);
+                    return ot.rc;
+                }
             }
             ECG_HIP(hipStreamWaitEvent(s_comp, c.out_done[slot], 0));  // slot's outputs copied out
         }
@@ -1688,7 +1697,10 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     }
     if (split) {
         ot.th.join();
-        if (ot.rc != ECG_OK) return ot.rc;
+        if (ot.rc != ECG_OK) {
+            set_last_error(ot.msg);
+            return ot.rc;
+        }
     }
     ECG_HIP(hipStreamSynchronize(s_out));
     return lease.done();
