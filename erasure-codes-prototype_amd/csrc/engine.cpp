@@ -1360,7 +1360,8 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         const unsigned seq = ++c.seq == 0 ? ++c.seq : c.seq;  // flags start at 0: never post 0
         int nflags = 0;
         for (const LinearOp& op : ops) {
-            const long long wg_max = ((B / 16 + kThreads - 1) / kThreads) * op.m_out();  // >= chunks x row tiles
+            // >= workgroups x row tiles of either latency kernel (4 bytes per lane is the finer grid)
+            const long long wg_max = ((B / 4 + kLatThreads - 1) / kLatThreads) * op.m_out();
             const bool f = flagged && nflags + wg_max <= kFlagSlots;
             flagged = f;
             int posted = 0;

@@ -152,6 +152,26 @@ __device__ __forceinline__ void fold(const uint32_t (&x)[U][4], const ECG_CONST 
     else fold_general<MT, U>(x, t, acc);
 }
 
+// Completion flag of a latency-kernel workgroup, for a polling host (vector stores only).  A system-scope
+// release is (1) the issuing wave's own stores complete (s_waitcnt vmcnt(0)), (2) the L2 written back
+// (buffer_wbl2, which covers the whole L2, not one wave's lines) and (3) that write-back complete before
+// the flag store.  So every wave waits for its own stores, the workgroup meets at a barrier, and only
+// lane 0 of wave 0 writes the L2 back and posts the flag: one L2 write-back per workgroup instead of one
+// per wave.  Step (3) is an explicit wait: after the barrier's vmcnt(0) the compiler's wait insertion
+// does not count the write-back as outstanding and drops the wait a release store would carry (seen
+// in the ISA: buffer_wbl2 directly followed by the flag store; a config-1 loopback run then read 3 of
+// 2617 rebuilt blocks stale).
+__device__ __forceinline__ void post_done_flag(const GfLaunch& a) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt / lgkmcnt unconstrained
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: buffer_wbl2
+        __builtin_amdgcn_s_waitcnt(0x0F70);            // the write-back has completed
+        __hip_atomic_store(a.done_flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // Minimum waves per EU the register allocator must allow (r01 sweep, tools/gpu_variants.sh): 8 for the
 // 1-2-output kernels (decode, repair, XOR: +2 % at 8 vs 6), 6 for 3-4 outputs (encode: 8 costs 1 %),
 // 4 above -- except 5 outputs: under the 128-VGPR cap of 4 waves the allocator spilled 12 bytes per lane
@@ -264,14 +284,56 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
             if (p < nrows) store16<NT>(dst[p] + off, acc[p]);
     }
     if constexpr (MODE == GF_MODE_INLINE_LAT) {
-        if (a.done_flags) {  // completion flag for a polling host (vector stores only)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's stores reach the host
-            __syncthreads();
-            if (threadIdx.x == 0)
-                __hip_atomic_store(a.done_flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq, __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (a.done_flags) post_done_flag(a);
     }
+}
+
+// Latency kernel for small zero-copy host calls (GF_MODE_INLINE_LAT, blocks <= ECG_OPT_LAT_DWORD_BYTES):
+// one DWORD column per lane instead of 16 bytes.  A 1 KiB call is 64 sixteen-byte columns, i.e. ONE wave
+// that runs the whole multiply (~550 VALU instructions per lane for RS(6,4)) after its PCIe loads; at 4
+// bytes per lane the same bytes are 256 lanes in 4 waves on 4 SIMDs, each with a quarter of the multiply.
+// KB = the input count rounded up to a bucket (k <= KB): straight-line code over KB inputs, so the
+// compiler issues every input load AND every coefficient-table scalar load up front.  With a runtime
+// `if (u < k)` per input each table fetch sat behind its own branch: k dependent L2 round trips after
+// the PCIe loads (~1.7 us of a 6.6 us kernel, rocprofv3 kernel trace vs the plain-copy probe).  Padded
+// inputs (u >= k) re-read input 0 with table 0 and are masked out of the sum.
+// kLatThreads dword columns per workgroup; grid.x = ceil((B / 4) / kLatThreads), grid.y = row tiles.
+template <int MT, bool BIN, int KB>
+__global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLaunch a) {
+    const int rt = blockIdx.y;
+    const int k = a.k;
+    const int row0 = rt * MT;
+    const int nrows = min(MT, a.m - row0);
+    const ECG_CONST CoefTab* T = cst(a.tabs) + (size_t)rt * (size_t)k * MT;
+    const long long ndw = a.B >> 2;
+    const long long c = (long long)blockIdx.x * kLatThreads + threadIdx.x;
+    if (c < ndw) {
+        const long long off = c << 2;
+        uint32_t x[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+            x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(a.isrc[u < k ? u : 0] + off));
+        uint32_t acc[MT];
+#pragma unroll
+        for (int p = 0; p < MT; ++p) acc[p] = 0u;
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const ECG_CONST CoefTab* t = T + (size_t)(u < k ? u : 0) * MT;
+            const uint32_t keep = u < k ? ~0u : 0u;  // uniform
+            if constexpr (BIN) {
+#pragma unroll
+                for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], x[u], t[p].mask & keep, 0x78);
+            } else {
+                const Split sp = split(x[u]);
+#pragma unroll
+                for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], gmul(t[p], sp), keep, 0x78);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < MT; ++p)
+            if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(a.idst[row0 + p] + off));
+    }
+    if (a.done_flags) post_done_flag(a);
 }
 
 // Byte path: bytes [off0, B) (tails, unaligned pointers).  cols_per_wg = bytes per workgroup.
@@ -347,6 +409,7 @@ void init_options() {
     g_opt[ECG_OPT_ZEROCOPY_BYTES].store(env("ECG_ZEROCOPY_BYTES", 8 << 20));
     g_opt[ECG_OPT_PROGRAM_CACHE].store(env("ECG_PROGRAM_CACHE", 4096));
     g_opt[ECG_OPT_MAP_GROUP].store(env("ECG_MAP_GROUP", 1));
+    g_opt[ECG_OPT_LAT_DWORD_BYTES].store(env("ECG_LAT_DWORD_BYTES", 32768));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -390,6 +453,39 @@ Launcher pick_vec(const GfLaunch& a, int nt) {
     }
 }
 
+template <int MT, bool BIN, int KB>
+void lat_dword_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
+    hipLaunchKernelGGL((gf_lat_dword_kernel<MT, BIN, KB>), g, dim3(kLatThreads), 0, st, a);
+}
+
+// input-count buckets of the latency kernel: exact for the BASELINE shapes (RS(6,4), RS(10,4) encode and
+// decode, Azure-LRC(12,2,2) global rows), at most 3 padded inputs elsewhere
+template <int MT, bool BIN>
+Launcher pick_lat_k(int k) {
+    if (k <= 4) return lat_dword_launch<MT, BIN, 4>;
+    if (k <= 6) return lat_dword_launch<MT, BIN, 6>;
+    if (k <= 8) return lat_dword_launch<MT, BIN, 8>;
+    if (k <= 10) return lat_dword_launch<MT, BIN, 10>;
+    if (k <= 12) return lat_dword_launch<MT, BIN, 12>;
+    if (k <= 16) return lat_dword_launch<MT, BIN, 16>;
+    return nullptr;
+}
+
+template <bool BIN>
+Launcher pick_lat_dword_bin(int MT, int k) {
+    switch (MT) {
+        case 1: return pick_lat_k<1, BIN>(k);
+        case 2: return pick_lat_k<2, BIN>(k);
+        case 3: return pick_lat_k<3, BIN>(k);
+        case 4: return pick_lat_k<4, BIN>(k);
+        case 5: return pick_lat_k<5, BIN>(k);
+        case 6: return pick_lat_k<6, BIN>(k);
+        case 7: return pick_lat_k<7, BIN>(k);
+        case 8: return pick_lat_k<8, BIN>(k);
+        default: return nullptr;
+    }
+}
+
 template <int MT, int MODE, bool BIN>
 void byte_launch(const GfLaunch& a, dim3 g, hipStream_t st) { launch_with(gf_byte_kernel<MT, MODE, BIN>, a, g, st); }
 
@@ -430,6 +526,7 @@ int set_option(int opt, long long value) {
     if (opt == ECG_OPT_ZEROCOPY_BYTES && value < 0) return -1;
     if (opt == ECG_OPT_PROGRAM_CACHE && value < 2) return -1;
     if (opt == ECG_OPT_MAP_GROUP && (value < 1 || value > (1 << 20))) return -1;
+    if (opt == ECG_OPT_LAT_DWORD_BYTES && value < 0) return -1;
     g_opt[opt].store(value);
     return 0;
 }
@@ -455,6 +552,18 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
     init_options();
     GfLaunch a = base;
     const long long vec_bytes = vec_ok ? (a.B & ~15LL) : 0;
+    if (mode == GF_MODE_INLINE_LAT && vec_bytes == a.B && a.B <= g_opt[ECG_OPT_LAT_DWORD_BYTES].load() &&
+        a.k <= kLatMaxSrc) {
+        // small zero-copy call: 4 bytes per lane (gf_lat_dword_kernel)
+        const long long gx = ((a.B >> 2) + kLatThreads - 1) / kLatThreads;
+        Launcher l = a.binary ? pick_lat_dword_bin<true>(a.MT, a.k) : pick_lat_dword_bin<false>(a.MT, a.k);
+        if (!l) return hipErrorInvalidValue;
+        l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (n_wg) *n_wg = (int)(gx * a.rtiles);
+        return hipSuccess;
+    }
     if (vec_bytes > 0) {
         const long long ncols = vec_bytes >> 4;
         long long cpw = g_opt[ECG_OPT_COLS_PER_WG].load();

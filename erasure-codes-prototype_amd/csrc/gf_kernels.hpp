@@ -40,6 +40,8 @@ constexpr int kMaxMT = 8;       // output rows per row tile
 #ifndef ECG_TPB
 #define ECG_TPB 128
 #endif
+constexpr int kLatThreads = 256;  // dword columns per workgroup of the small-call latency kernel
+constexpr int kLatMaxSrc = 16;    // inputs it loads up front
 constexpr int kThreads = ECG_TPB;  // threads per workgroup (2 waves of 64, r01 tuning); ECG_TPB only for tuning builds
 
 struct GfLaunch {

@@ -38,7 +38,8 @@ ECG_OPT_GRID_MAP = 2
 ECG_OPT_ZEROCOPY_BYTES = 3
 ECG_OPT_PROGRAM_CACHE = 4
 ECG_OPT_MAP_GROUP = 5
-ECG_OPT_COUNT = 6
+ECG_OPT_LAT_DWORD_BYTES = 6
+ECG_OPT_COUNT = 7
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 

@@ -52,7 +52,8 @@ int ecg_program_sets_retiring(void);
 int ecg_host_contexts(void);
 
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
- * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP, ECG_MAP_GROUP).  Results never depend on them. */
+ * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP, ECG_ZEROCOPY_BYTES, ECG_PROGRAM_CACHE, ECG_MAP_GROUP,
+ * ECG_LAT_DWORD_BYTES).  Results never depend on them. */
 #define ECG_OPT_NT 0           /* non-temporal policy: bit 0 = loads, bit 1 = stores (default 3) */
 #define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 128; 0 = auto (128 = 2 KiB) */
 #define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous, 2 = stripe s on XCD group s%8,
@@ -67,7 +68,11 @@ int ecg_host_contexts(void);
                                    Default 4096 */
 #define ECG_OPT_MAP_GROUP 5    /* grid map 2: adjacent stripes per XCD group run (default 1 = stripe s on
                                   group s % 8); reduced to a power-of-two divisor tiling S when needed */
-#define ECG_OPT_COUNT 6
+#define ECG_OPT_LAT_DWORD_BYTES 6 /* zero-copy host calls with blocks of at most this many bytes run the
+                                     latency kernel with 4 bytes per lane (more waves share the multiply);
+                                     0 = never; default 32768 (measured: 4 bytes per lane is faster up to
+                                     32 KiB, equal at 64-256 KiB; profiles/r02/lat_kernel/) */
+#define ECG_OPT_COUNT 7
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

@@ -210,6 +210,9 @@ def test_tuning_options_validation(ecg):
         assert ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE) == saved[ecg.ECG_OPT_PROGRAM_CACHE]
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_COLS_PER_WG, 512) == 0
         assert ecg.get_option(ecg.ECG_OPT_COLS_PER_WG) == 512
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, -1) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, 0) == 0  # 16 bytes per lane always
+        assert ecg.get_option(ecg.ECG_OPT_LAT_DWORD_BYTES) == 0
     finally:
         for o, v in enumerate(saved):
             ecg.set_option(o, v)
@@ -217,6 +220,8 @@ def test_tuning_options_validation(ecg):
         assert saved[ecg.ECG_OPT_GRID_MAP] == 3  # auto
     if "ECG_MAP_GROUP" not in os.environ:
         assert saved[ecg.ECG_OPT_MAP_GROUP] == 1
+    if "ECG_LAT_DWORD_BYTES" not in os.environ:
+        assert saved[ecg.ECG_OPT_LAT_DWORD_BYTES] == 32768
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])

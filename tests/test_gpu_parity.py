@@ -64,6 +64,59 @@ def test_matrix_encode_random_matrices(ecg, oracle, torch_cuda):
         assert same(a, b), (k, m, M)
 
 
+@pytest.mark.parametrize("lat_dword", [None, 0, 1 << 20])
+def test_latency_kernel_shapes(ecg, oracle, torch_cuda, lat_dword):
+    """Zero-copy host calls at 16-byte multiples: the 4-bytes-per-lane latency kernel (blocks up to
+    ECG_OPT_LAT_DWORD_BYTES; every input-count bucket 4/6/8/10/12/16 with padded inputs, GENERAL and
+    BINARY, row tiles) and the 16-byte latency kernel above it, each call checked at once; at the
+    default threshold, with the 16-byte kernel only (0) and with the 4-byte kernel only (1 MiB)."""
+    saved = ecg.get_option(ecg.ECG_OPT_LAT_DWORD_BYTES)
+    if lat_dword is not None:
+        ecg.set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, lat_dword)
+    try:
+        _latency_kernel_shapes(ecg, oracle)
+    finally:
+        ecg.set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, saved)
+
+
+def _latency_kernel_shapes(ecg, oracle):
+    rng = random.Random(11)
+    for B in (16, 1024, 4096, 16384, 16400, 32768, 32784):
+        for k in range(1, 19):
+            m = rng.randint(1, 9)
+            kind = rng.randrange(3)
+            if kind == 0:
+                M = [rng.randrange(256) for _ in range(k * m)]
+            elif kind == 1:
+                M = [rng.randrange(2) for _ in range(k * m)]  # BINARY flavour
+            else:
+                M = oracle.reed_sol_vandermonde_coding_matrix(k, m) if k + m <= 256 else [1] * (k * m)
+            data = [rnd(B, 7000 + 31 * k + j + B) for j in range(k)]
+            a = [rnd(B, 800 + i) for i in range(m)]
+            b = [x.copy() for x in a]
+            oracle.jerasure_matrix_encode(k, m, M, data, a, B)
+            ecg.jerasure_matrix_encode(k, m, M, data, b, B)
+            assert same(a, b), (B, k, m, kind)
+
+
+def test_flagged_calls_never_read_stale(ecg, oracle, torch_cuda):
+    """3000 back-to-back RS(6,4) 1 KiB and RS(12,4) 4 KiB host calls with fresh data every call: each
+    call's parities are compared before the next call (a completion flag posted before the outputs
+    reach host memory shows up here as stale bytes)."""
+    for k, m, B, n in ((6, 4, 1024, 2000), (12, 4, 4096, 1000)):
+        M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+        rng = np.random.default_rng(k)
+        out = [np.zeros(B, np.uint8) for _ in range(m)]
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        bad = 0
+        for i in range(n):
+            data = list(rng.integers(0, 256, (k, B), dtype=np.uint8))
+            ecg.jerasure_matrix_encode(k, m, M, data, out, B)
+            oracle.jerasure_matrix_encode(k, m, M, data, ref, B)
+            bad += not same(out, ref)
+        assert bad == 0, (k, m, B, bad)
+
+
 @pytest.mark.parametrize("k,m,row_k_ones", [(6, 4, 1), (6, 4, 0), (10, 4, 1), (4, 2, 1)])
 def test_matrix_decode_host_all_patterns(ecg, oracle, torch_cuda, k, m, row_k_ones):
     B = 1024 + 7

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--sweep-zc", action="store_true",
                     help="zero-copy threshold sweep: RS(10,4) 32-256 KiB blocks, DMA staging vs zero-copy")
+    ap.add_argument("--sweep-lat", action="store_true",
+                    help="latency-kernel lane width: RS(10,4) 1-256 KiB zero-copy calls, 4 vs 16 bytes per lane")
     a = ap.parse_args()
     rng = np.random.default_rng(0)
     res = {}
@@ -37,8 +39,15 @@ def main():
              [(6, 4, 1024), (10, 4, 1024), (10, 4, 16384), (10, 4, 65536), (10, 4, 1 << 20)]]
     if a.sweep_zc:
         cases = [(zc, 10, 4, B) for B in (32768, 65536, 98304, 131072, 196608, 262144) for zc in (0, 1 << 26)]
+    lat = {}
+    if a.sweep_lat:  # zc slot carries the ECG_OPT_LAT_DWORD_BYTES value; zero-copy stays at its default
+        cases = [(lw, 10, 4, B) for r in range(2) for B in (1024, 4096, 16384, 32768, 65536, 131072, 262144)
+                 for lw in (0, 1 << 20)]
     for zc, k, m, B in cases:
-        ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, zc)
+        if a.sweep_lat:
+            ecg.set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, zc)
+        else:
+            ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, zc)
         M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
         data = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(k)]
         coding = [np.zeros(B, np.uint8) for _ in range(m)]
@@ -46,7 +55,9 @@ def main():
         enc = per_call(lambda: ecg.jerasure_matrix_encode(k, m, M, data, coding, B), n)
         er = [3, -1]
         dec = per_call(lambda: ecg.jerasure_matrix_decode(k, m, M, 1, er, data, coding, B), n)
-        name = f"RS({k},{m}) B={B} zerocopy<={zc}"
+        name = f"RS({k},{m}) B={B} " + (f"lat_dword<={zc}" if a.sweep_lat else f"zerocopy<={zc}")
+        if name in res:
+            name += " (round 2)"
         res[name] = {"encode_us": round(enc, 1), "decode_us": round(dec, 1),
                      "encode_GBps_data": round(k * B / enc / 1e3, 3)}
         print(f"{name:40s} encode {enc:9.1f} us/call   decode {dec:9.1f} us/call", flush=True)

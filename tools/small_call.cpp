@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "ecg.h"
@@ -98,6 +99,55 @@ __global__ void touch_parallel_flag_kernel(const uint4* in, uint4* out, unsigned
     }
 #pragma unroll
     for (int p = 0; p < M; p++) out[p * 64 + lane] = acc;
+    publish(flag, seq);
+}
+
+// parF with the product's kernel-argument size: the pointers travel in a ~1.5 KiB struct (GfLaunch
+// carries 128 input + 32 output inline pointers), to see what a large kernarg block costs per launch
+struct BigArgs {
+    const uint4* in;
+    uint4* out;
+    unsigned* flag;
+    unsigned seq;
+    const void* pad[180];
+};
+
+__global__ void touch_parallel_flag_big_kernel(const BigArgs a) {
+    const int lane = threadIdx.x;
+    uint4 v[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) v[j] = a.in[j * 64 + lane];
+    uint4 acc = v[0];
+#pragma unroll
+    for (int j = 1; j < 6; j++) {
+        acc.x ^= v[j].x;
+        acc.y ^= v[j].y;
+        acc.z ^= v[j].z;
+        acc.w ^= v[j].w;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) a.out[p * 64 + lane] = acc;
+    publish(a.flag, a.seq);
+}
+
+// parF plus 24 coefficient words read from a device-memory table through scalar loads (the product
+// kernel's CoefTab fetch), folded into the result so the loads cannot be dropped
+__global__ void touch_parallel_flag_tab_kernel(const uint4* in, uint4* out, const __attribute__((address_space(4))) unsigned* tab,
+                                               unsigned* flag, unsigned seq) {
+    const int lane = threadIdx.x;
+    uint4 v[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) v[j] = in[j * 64 + lane];
+    uint4 acc = v[0];
+#pragma unroll
+    for (int j = 1; j < 6; j++) {
+        acc.x ^= v[j].x & tab[j * 8];
+        acc.y ^= v[j].y & tab[j * 8 + 1];
+        acc.z ^= v[j].z & tab[j * 8 + 2];
+        acc.w ^= v[j].w & tab[j * 8 + 3];
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) out[p * 64 + lane] = acc;
     publish(flag, seq);
 }
 
@@ -189,7 +239,51 @@ int main(int argc, char** argv) {
         spin(hflag, seq, st);
         CK(hipStreamSynchronize(st));
     });
+    BigArgs big{};
+    big.in = (const uint4*)d;
+    big.out = (uint4*)(d + (size_t)k * B);
+    big.flag = dflag;
+    bench("parFbig", [&] {
+        big.seq = ++seq;
+        hipLaunchKernelGGL(touch_parallel_flag_big_kernel, dim3(1), dim3(64), 0, st, big);
+        spin(hflag, seq, st);
+    });
+    unsigned* dtab = nullptr;
+    CK(hipMalloc((void**)&dtab, 4096));
+    CK(hipMemset(dtab, 0xff, 4096));
+    CK(hipDeviceSynchronize());
+    bench("parFtab", [&] {
+        ++seq;
+        hipLaunchKernelGGL(touch_parallel_flag_tab_kernel, dim3(1), dim3(64), 0, st, (const uint4*)d,
+                           (uint4*)(d + (size_t)k * B), (const __attribute__((address_space(4))) unsigned*)dtab, dflag, seq);
+        spin(hflag, seq, st);
+    });
+    // parF plus the call's host-side gather into staging and scatter back (6 KiB in, 4 KiB out)
+    bench("parFcp", [&] {
+        ++seq;
+        for (int i = 0; i < k; i++) memcpy(h + (size_t)i * B, p[i], B);
+        hipLaunchKernelGGL((touch_parallel_flag_kernel<6, 4>), dim3(1), dim3(64), 0, st, (const uint4*)d,
+                           (uint4*)(d + (size_t)k * B), dflag, seq);
+        spin(hflag, seq, st);
+        for (int i = 0; i < m; i++) memcpy(p[k + i], h + (size_t)(k + i) * B, B);
+    });
+    // A/B of the latency kernel's lane width (ECG_OPT_LAT_DWORD_BYTES: 4 bytes per lane vs 16), alternated
+    const long long lat_default = ecg_get_option(ECG_OPT_LAT_DWORD_BYTES);
+    int erasures[3] = {2, -1, -1};
+    for (int r = 0; r < 2; r++) {
+        for (long long opt : {lat_default, 0LL}) {
+            ecg_set_option(ECG_OPT_LAT_DWORD_BYTES, opt);
+            bench(opt ? "callD" : "call16", [&] {
+                if (ecg_jerasure_matrix_encode(k, m, 8, M, p.data(), p.data() + k, B) != 0) exit(2);
+            });
+            bench(opt ? "decD" : "dec16", [&] {
+                if (ecg_jerasure_matrix_decode(k, m, 8, M, 1, erasures, p.data(), p.data() + k, B) != 0) exit(2);
+            });
+        }
+    }
+    ecg_set_option(ECG_OPT_LAT_DWORD_BYTES, lat_default);
     CK(hipStreamSynchronize(st));
+    CK(hipFree(dtab));
     CK(hipHostFree(hflag));
     ecg_free(M);
     CK(hipHostFree(h));
