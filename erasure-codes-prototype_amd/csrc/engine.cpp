@@ -452,7 +452,10 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     ps->used_on(st);
     a.done_flags = latency ? flags : nullptr;
     a.done_seq = seq;
-    ECG_HIP(launch_gf(a, latency ? GF_MODE_INLINE_LAT : GF_MODE_INLINE, vec_ok, st, n_flags));
+    // A single small call fills a few dozen workgroups: its time is the latency chain, not bandwidth, so
+    // small blocks take the latency kernel (every load in flight at once) on the device tier as well.
+    const bool lat = latency || (B <= get_option(ECG_OPT_LAT_DWORD_BYTES) && op.k_in() <= kLatMaxSrc);
+    ECG_HIP(launch_gf(a, lat ? GF_MODE_INLINE_LAT : GF_MODE_INLINE, vec_ok, st, n_flags));
     return ECG_OK;
 }
 

@@ -409,7 +409,7 @@ void init_options() {
     g_opt[ECG_OPT_ZEROCOPY_BYTES].store(env("ECG_ZEROCOPY_BYTES", 8 << 20));
     g_opt[ECG_OPT_PROGRAM_CACHE].store(env("ECG_PROGRAM_CACHE", 4096));
     g_opt[ECG_OPT_MAP_GROUP].store(env("ECG_MAP_GROUP", 1));
-    g_opt[ECG_OPT_LAT_DWORD_BYTES].store(env("ECG_LAT_DWORD_BYTES", 32768));
+    g_opt[ECG_OPT_LAT_DWORD_BYTES].store(env("ECG_LAT_DWORD_BYTES", 1 << 20));
     g_opt_init.store(1, std::memory_order_release);
 }
 

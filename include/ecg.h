@@ -68,10 +68,10 @@ int ecg_host_contexts(void);
                                    Default 4096 */
 #define ECG_OPT_MAP_GROUP 5    /* grid map 2: adjacent stripes per XCD group run (default 1 = stripe s on
                                   group s % 8); reduced to a power-of-two divisor tiling S when needed */
-#define ECG_OPT_LAT_DWORD_BYTES 6 /* zero-copy host calls with blocks of at most this many bytes run the
-                                     latency kernel with 4 bytes per lane (more waves share the multiply);
-                                     0 = never; default 32768 (measured: 4 bytes per lane is faster up to
-                                     32 KiB, equal at 64-256 KiB; profiles/r02/lat_kernel/) */
+#define ECG_OPT_LAT_DWORD_BYTES 6 /* single calls (one stripe: host tier, or the device tier outside a batch
+                                     scope) with blocks of at most this many bytes run the latency kernel:
+                                     4 bytes per lane, every input load in flight at once; 0 = never;
+                                     default 1 MiB (profiles/r02/lat_kernel/) */
 #define ECG_OPT_COUNT 7
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);

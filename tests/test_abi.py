@@ -221,7 +221,7 @@ def test_tuning_options_validation(ecg):
     if "ECG_MAP_GROUP" not in os.environ:
         assert saved[ecg.ECG_OPT_MAP_GROUP] == 1
     if "ECG_LAT_DWORD_BYTES" not in os.environ:
-        assert saved[ecg.ECG_OPT_LAT_DWORD_BYTES] == 32768
+        assert saved[ecg.ECG_OPT_LAT_DWORD_BYTES] == 1 << 20
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])

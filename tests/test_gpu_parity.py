@@ -592,6 +592,37 @@ def test_cauchy_local_decode_quirk(ecg, oracle, torch_cuda, t):
 
 # ------------------------------------------------------------------ device tier + batches
 
+@pytest.mark.parametrize("lat_dword", [None, 0])
+def test_device_tier_single_call_latency_kernel(ecg, oracle, torch_cuda, lat_dword):
+    """Single device-tier calls with blocks up to ECG_OPT_LAT_DWORD_BYTES run the latency kernel (4 bytes
+    per lane, every input-count bucket, padded inputs masked); above it, or with the option at 0, the
+    bulk kernel.  Both against the oracle, back to back on one stream, then one synchronize."""
+    torch = torch_cuda
+    saved = ecg.get_option(ecg.ECG_OPT_LAT_DWORD_BYTES)
+    if lat_dword is not None:
+        ecg.set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, lat_dword)
+    try:
+        rng = random.Random(5)
+        cases = []
+        for B in (1024, 65536, 1 << 20, (1 << 20) + 16):
+            for k in (1, 3, 5, 6, 7, 10, 12, 13, 16, 17):
+                m = rng.randint(1, 9)
+                M = ([rng.randrange(2) for _ in range(k * m)] if k % 2 else
+                     [rng.randrange(256) for _ in range(k * m)])
+                host = [rnd(B, 300 * k + j + B) for j in range(k)]
+                dev_data = [torch.from_numpy(h).cuda() for h in host]
+                dev_cod = [torch.zeros(B, dtype=torch.uint8, device="cuda") for _ in range(m)]
+                ecg.dev_matrix_encode(k, m, M, dev_data, dev_cod, B)
+                cases.append((B, k, m, M, host, dev_cod))
+        torch.cuda.synchronize()
+        for B, k, m, M, host, dev_cod in cases:
+            ref = [np.zeros(B, np.uint8) for _ in range(m)]
+            oracle.jerasure_matrix_encode(k, m, M, host, ref, B)
+            assert same([c.cpu().numpy() for c in dev_cod], ref), (B, k, m)
+    finally:
+        ecg.set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, saved)
+
+
 def test_device_tier_aligned_and_unaligned(ecg, oracle, torch_cuda):
     torch = torch_cuda
     k, m = 10, 4
