@@ -8,6 +8,14 @@
 //            lane per block, like the product kernel) + synchronize: empty + the PCIe traffic
 //   par      the same with all six loads issued before the first use (one PCIe round trip)
 //   read1    one 1 KiB block read, four written;   write   four written, nothing read
+//   emptyF / parF   empty / par, completing by a flag the kernel posts in mapped host memory (host polls)
+//   parFbig  parF with the product's ~1.5 KiB kernel-argument block (no measurable cost)
+//   parFtab  parF plus 24 coefficient words read through scalar loads from a device table (no cost
+//            when the loads are not behind per-input branches)
+//   parFcp   parF plus the call's host-side gather (6 KiB) and scatter (4 KiB) memcpys: the floor of a
+//            zero-copy call
+//   callD / call16, decD / dec16   the product's encode / decode with the latency kernel at 4 bytes
+//            per lane (ECG_OPT_LAT_DWORD_BYTES default) and at 16 bytes per lane (option 0), alternated
 // Run under rocprofv3 --kernel-trace --hip-trace --stats to split each into API and kernel time.
 // Build: hipcc -O2 -std=c++20 --offload-arch=gfx950 -Iinclude tools/small_call.cpp -Lerasure-codes-prototype_amd/lib -lecg
 //        -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o tools/small_call
