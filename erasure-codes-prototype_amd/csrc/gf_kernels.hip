@@ -299,6 +299,33 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
 // inputs (u >= k) re-read input 0 with table 0 and are masked out of the sum.
 // kLatThreads dword columns per workgroup; grid.x = ceil((B / 4) / kLatThreads), grid.y = row tiles.
 template <int MT, bool BIN, int KB>
+__device__ __forceinline__ void lat_fold(const GfLaunch& a, const ECG_CONST CoefTab* T, const uint32_t (&x)[KB],
+                                         uint32_t (&acc)[MT]) {
+    const int k = a.k;
+#pragma unroll
+    for (int p = 0; p < MT; ++p) acc[p] = 0u;
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+        const ECG_CONST CoefTab* t = T + (size_t)(u < k ? u : 0) * MT;
+        const uint32_t keep = u < k ? ~0u : 0u;  // uniform
+        if constexpr (BIN) {
+#pragma unroll
+            for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], x[u], t[p].mask & keep, 0x78);
+        } else {
+            const Split sp = split(x[u]);
+#pragma unroll
+            for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], gmul(t[p], sp), keep, 0x78);
+        }
+    }
+}
+
+// EAGER (blocks <= kLatEagerBytes): lanes past the end load the last column and store nothing, so no
+// branch precedes the loads (block size, pointers and k come in fewer rounds of kernel-argument loads),
+// every pointer slot is loaded and then selected (no wait for k), and a scheduling barrier issues every
+// input load before the first coefficient-table load.  RS(6,4) 1 KiB host calls 0.3-2 us faster (A/B
+// of two builds over two boxes, profiles/r02/lat_kernel/eager/); single device calls at 64 KiB - 1 MiB
+// measured 1-5 % slower with it (the barrier raises register use), so only small blocks take it.
+template <int MT, bool BIN, int KB, bool EAGER>
 __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLaunch a) {
     const int rt = blockIdx.y;
     const int k = a.k;
@@ -307,28 +334,31 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLa
     const ECG_CONST CoefTab* T = cst(a.tabs) + (size_t)rt * (size_t)k * MT;
     const long long ndw = a.B >> 2;
     const long long c = (long long)blockIdx.x * kLatThreads + threadIdx.x;
-    if (c < ndw) {
+    if constexpr (EAGER) {
+        const bool live = c < ndw;
+        const long long off = (live ? c : ndw - 1) << 2;
+        uint32_t x[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const uint8_t* pu = a.isrc[u];  // a.isrc has kInlineSrc >= KB slots, the unused ones zeroed
+            x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>((u < k ? pu : a.isrc[0]) + off));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t acc[MT];
+        lat_fold<MT, BIN, KB>(a, T, x, acc);
+        if (live) {
+#pragma unroll
+            for (int p = 0; p < MT; ++p)
+                if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(a.idst[row0 + p] + off));
+        }
+    } else if (c < ndw) {
         const long long off = c << 2;
         uint32_t x[KB];
 #pragma unroll
         for (int u = 0; u < KB; ++u)
             x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(a.isrc[u < k ? u : 0] + off));
         uint32_t acc[MT];
-#pragma unroll
-        for (int p = 0; p < MT; ++p) acc[p] = 0u;
-#pragma unroll
-        for (int u = 0; u < KB; ++u) {
-            const ECG_CONST CoefTab* t = T + (size_t)(u < k ? u : 0) * MT;
-            const uint32_t keep = u < k ? ~0u : 0u;  // uniform
-            if constexpr (BIN) {
-#pragma unroll
-                for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], x[u], t[p].mask & keep, 0x78);
-            } else {
-                const Split sp = split(x[u]);
-#pragma unroll
-                for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], gmul(t[p], sp), keep, 0x78);
-            }
-        }
+        lat_fold<MT, BIN, KB>(a, T, x, acc);
 #pragma unroll
         for (int p = 0; p < MT; ++p)
             if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(a.idst[row0 + p] + off));
@@ -455,7 +485,8 @@ Launcher pick_vec(const GfLaunch& a, int nt) {
 
 template <int MT, bool BIN, int KB>
 void lat_dword_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
-    hipLaunchKernelGGL((gf_lat_dword_kernel<MT, BIN, KB>), g, dim3(kLatThreads), 0, st, a);
+    if (a.B <= kLatEagerBytes) hipLaunchKernelGGL((gf_lat_dword_kernel<MT, BIN, KB, true>), g, dim3(kLatThreads), 0, st, a);
+    else hipLaunchKernelGGL((gf_lat_dword_kernel<MT, BIN, KB, false>), g, dim3(kLatThreads), 0, st, a);
 }
 
 // input-count buckets of the latency kernel: exact for the BASELINE shapes (RS(6,4), RS(10,4) encode and

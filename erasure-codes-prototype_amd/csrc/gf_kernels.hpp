@@ -42,6 +42,7 @@ constexpr int kMaxMT = 8;       // output rows per row tile
 #endif
 constexpr int kLatThreads = 256;  // dword columns per workgroup of the small-call latency kernel
 constexpr int kLatMaxSrc = 16;    // inputs it loads up front
+constexpr long long kLatEagerBytes = 16 << 10;  // blocks up to this size take its EAGER form
 constexpr int kThreads = ECG_TPB;  // threads per workgroup (2 waves of 64, r01 tuning); ECG_TPB only for tuning builds
 
 struct GfLaunch {

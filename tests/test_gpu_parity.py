@@ -604,7 +604,7 @@ def test_device_tier_single_call_latency_kernel(ecg, oracle, torch_cuda, lat_dwo
     try:
         rng = random.Random(5)
         cases = []
-        for B in (1024, 65536, 1 << 20, (1 << 20) + 16):
+        for B in (1024, 65536, 65552, 262144, 1 << 20, (1 << 20) + 16):
             for k in (1, 3, 5, 6, 7, 10, 12, 13, 16, 17):
                 m = rng.randint(1, 9)
                 M = ([rng.randrange(2) for _ in range(k * m)] if k % 2 else
