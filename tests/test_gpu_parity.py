@@ -100,21 +100,28 @@ def _latency_kernel_shapes(ecg, oracle):
 
 
 def test_flagged_calls_never_read_stale(ecg, oracle, torch_cuda):
-    """3000 back-to-back RS(6,4) 1 KiB and RS(12,4) 4 KiB host calls with fresh data every call: each
-    call's parities are compared before the next call (a completion flag posted before the outputs
-    reach host memory shows up here as stale bytes)."""
-    for k, m, B, n in ((6, 4, 1024, 2000), (12, 4, 4096, 1000)):
+    """Back-to-back host calls with fresh data every call -- RS(6,4) 1 KiB, RS(12,4) 4 KiB, RS(10,4)
+    16 KiB (16 workgroups, 16 flags per output tile) encodes, every fourth followed by a decode: each
+    call's output is compared before the next call (a completion flag posted before the outputs reach
+    host memory shows up here as stale bytes)."""
+    for k, m, B, n in ((6, 4, 1024, 2000), (12, 4, 4096, 1000), (10, 4, 16384, 300)):
         M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
         rng = np.random.default_rng(k)
         out = [np.zeros(B, np.uint8) for _ in range(m)]
         ref = [np.zeros(B, np.uint8) for _ in range(m)]
-        bad = 0
+        bad = bad_dec = 0
         for i in range(n):
             data = list(rng.integers(0, 256, (k, B), dtype=np.uint8))
             ecg.jerasure_matrix_encode(k, m, M, data, out, B)
             oracle.jerasure_matrix_encode(k, m, M, data, ref, B)
             bad += not same(out, ref)
-        assert bad == 0, (k, m, B, bad)
+            if i % 4 == 0:  # and a decode of one lost data block, from fresh survivors
+                lost = i % k
+                d = [x.copy() for x in data]
+                d[lost][:] = 0
+                ecg.jerasure_matrix_decode(k, m, M, 1, [lost, -1], d, [x.copy() for x in ref], B)
+                bad_dec += not np.array_equal(d[lost], data[lost])
+        assert bad == 0 and bad_dec == 0, (k, m, B, bad, bad_dec)
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(6, 4, 1), (6, 4, 0), (10, 4, 1), (4, 2, 1)])
