@@ -9,6 +9,11 @@ Default workload (BASELINE.json configs[1], what the driver runs):
        (row_k_ones = failed_num, rs.cpp:36) into the rebuild buffer  (ecg_decode_batch, 14 patterns)
   value = N * S * 2 * k * B / t_max in GiB/s (each pass reads k data-sized blocks per stripe).
   Inputs: splitmix64 bytes generated on the GPU before the timed region.
+  The same line also carries, after the headline's buffers are freed:
+    per_rank  every rank's encode / decode kernel time and HBM fraction (all-gathered);
+    config5   BASELINE.json configs[4] at this N: RS(10,4), 4 MiB, 65536 stripes sharded over the ranks
+              in HBM-resident waves of 1024 -- aggregate GiB/s, every rank's HBM fraction, and the
+              combined parity checksum against the N = 1 value (--no-config5 skips it).
 
 Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line):
   lrc-repair  configs[2]: Azure-LRC(12,2,2), 1 MiB, single-block repair of block s mod 16 of every
@@ -48,6 +53,12 @@ import ecg_dist as D  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 METRIC = "GiB/s encode + single-block decode (device-resident), RS(10,4) 1 MiB blocks, 1 & 8 GPU"
+# BASELINE.json configs[4]: RS(10,4), 4 MiB blocks, 65536 stripes sharded over the GPUs, encoded in
+# HBM-resident waves of 1024 stripes.  Its combined parity checksum does not depend on the sharding; the
+# N = 1 value of the full batch (profiles/r02/workloads/bench_rs4m-waves.log) is the bit-exact check at N > 1.
+CONFIG5_STRIPES, CONFIG5_BLOCK, CONFIG5_WAVE = 65536, 4 << 20, 1024
+CONFIG5_CHECKSUM_N1 = 0x3B120CA5EC06F46F
+LAUNCH_TIMEOUT_S = 1200.0
 
 
 def parse():
@@ -66,6 +77,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--launch-check", action="store_true",
                     help="rank bookkeeping only (gloo, no GPU): each rank reports itself, rank 0 prints one line")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="default workload: skip the config-5 sub-object (RS(10,4) 4 MiB waves) of the line")
+    ap.add_argument("--config5-stripes", type=int, default=CONFIG5_STRIPES,
+                    help="config 5's global stripe count, sharded over the ranks (BASELINE: 65536)")
+    ap.add_argument("--config5-block-size", type=int, default=CONFIG5_BLOCK)
+    ap.add_argument("--timeout", type=float, default=LAUNCH_TIMEOUT_S,
+                    help="--gpus N > 1 started outside torch.distributed: wall-clock limit (s) on the ranks; "
+                         "past it every rank is killed and bench.py exits 124")
     return ap.parse_args()
 
 
@@ -73,24 +92,56 @@ def launch_ranks(a) -> int:
     """`--gpus N` (N > 1) without a torch.distributed environment: start N fresh rank processes with
     torch.distributed.run as a CHILD process (this process never touches the GPU and never exec()s),
     forward their output, relay rank 0's JSON line on stdout, and return non-zero if any rank failed or
-    rank 0 printed no line.  Each rank re-runs this file with the same arguments; it sees WORLD_SIZE = N."""
+    rank 0 printed no line.  Each rank re-runs this file with the same arguments; it sees WORLD_SIZE = N.
+
+    Watchdog: the child runs in its own process group; if it is still running after `--timeout` seconds
+    (a rank stuck in RCCL init or a collective, a hung kernel), the whole group gets SIGTERM, then SIGKILL
+    10 s later, and this returns 124.  The ranks' own limit is ecg_dist's init/collective timeout."""
+    import signal
     import socket
     import subprocess
+    import threading
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    fired = threading.Event()
+
+    def kill_group(sig):
+        try:
+            os.killpg(p.pid, sig)  # the group this call started (start_new_session: pgid == p.pid)
+        except ProcessLookupError:
+            pass
+
+    def expire():
+        if p.poll() is None:
+            fired.set()
+            print(f"bench.py: ranks still running after {a.timeout:.0f} s: terminating them", file=sys.stderr)
+            kill_group(signal.SIGTERM)
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                kill_group(signal.SIGKILL)
+
+    timer = threading.Timer(a.timeout, expire)
+    timer.daemon = True
+    timer.start()
     lines = []
-    for ln in p.stdout:
-        if ln.startswith("{"):
-            lines.append(ln.strip())
-        else:
-            sys.stderr.write(ln)
-            sys.stderr.flush()
-    rc = p.wait()
+    try:
+        for ln in p.stdout:
+            if ln.startswith("{"):
+                lines.append(ln.strip())
+            else:
+                sys.stderr.write(ln)
+                sys.stderr.flush()
+        rc = p.wait()
+    finally:
+        timer.cancel()
+    if fired.is_set():
+        return 124
     if rc != 0:
         print(f"bench.py: {a.gpus} ranks under torch.distributed.run exited with status {rc}", file=sys.stderr)
         return rc
@@ -290,9 +341,59 @@ def rs_encode_decode(a, r):
                      "decode_traffic": pmc_traffic("decode", f"rs{k}{m}_B{B}_S{S}")},
         "parity_checksums": [f"{c:016x}" for c in checks],
     }
+    # every rank's own kernel times and HBM fractions (HIP events on its stream), not rank 0's only
+    mine = [enc_avg * 1e3, dec_avg * 1e3, achieved / HBM_PEAK_GBS, dec_bytes / dec_avg / 1e9 / HBM_PEAK_GBS]
+    per = D.gather_floats(mine, r, device="cuda")
+    line["per_rank"] = {"encode_ms": [round(x[0], 3) for x in per], "decode_ms": [round(x[1], 3) for x in per],
+                        "encode_frac": [round(x[2], 4) for x in per], "decode_frac": [round(x[3], 4) for x in per],
+                        "encode_frac_min": round(min(x[2] for x in per), 4),
+                        "encode_frac_max": round(max(x[2] for x in per), 4),
+                        "decode_frac_min": round(min(x[3] for x in per), 4),
+                        "decode_frac_max": round(max(x[3] for x in per), 4)}
+    # the headline's buffers go before config 5 allocates its wave
+    del stripes, rebuilt, data, coding, pattern_of_stripe, idx, step, evs
+    torch.cuda.empty_cache()
+    if not a.no_config5:
+        line["config5"] = config5(a, r, M, k, m)
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line
+
+
+def config5(a, r, M, k, m):
+    """BASELINE.json configs[4] inside the default line, at every N: RS(10,4), 4 MiB blocks, 65536 global
+    stripes sharded over the ranks as contiguous ranges (D.stripe_range; the coordinator fanning stripes
+    out to proxies, repair.cpp:112-132 / proxy.cpp:312-399), encoded in HBM-resident waves of 1024
+    stripes whose input is regenerated on device outside the timing (encode_waves).  Aggregate = all
+    ranks' data / the slowest rank's summed encode time; every rank's HBM fraction is all-gathered; the
+    per-rank parity checksums combine to a value that must equal the N = 1 one."""
+    B, total = a.config5_block_size, a.config5_stripes
+    n = k + m
+    first, last = D.stripe_range(total, r)
+    D.barrier(r)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_s, checks = encode_waves(k, m, M, B, first, last, CONFIG5_WAVE)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    frac = (last - first) * n * B / kernel_s / 1e9 / HBM_PEAK_GBS if kernel_s > 0 else 0.0
+    per = D.gather_floats([last - first, kernel_s, frac, wall], r, device="cuda")
+    sums = D.gather_checksums(checks, r, device="cuda")
+    t_max = max(x[1] for x in per)
+    combined = D.combine(sums)
+    full = total == CONFIG5_STRIPES and B == CONFIG5_BLOCK
+    return {"workload": f"RS({k},{m}) {B >> 20} MiB encode, {total} stripes over {r.world} GPU(s), "
+                        f"waves of {CONFIG5_WAVE} (BASELINE configs[4])",
+            "aggregate_GiBps": round(total * k * B / t_max / 2 ** 30, 1) if t_max > 0 else None,
+            "encode_seconds_max": round(t_max, 4),
+            "wall_seconds_max_incl_regeneration": round(max(x[3] for x in per), 3),
+            "stripes_per_rank": [int(x[0]) for x in per],
+            "hbm_frac_per_rank": [round(x[2], 4) for x in per],
+            "hbm_frac_min": round(min(x[2] for x in per), 4), "hbm_frac_max": round(max(x[2] for x in per), 4),
+            "algorithmic_bytes_per_stripe": n * B,
+            "parity_checksum": f"{combined:016x}",
+            "parity_checksum_n1": f"{CONFIG5_CHECKSUM_N1:016x}" if full else None,
+            "checksum_equals_n1": (combined == CONFIG5_CHECKSUM_N1) if full else None}
 
 
 # ------------------------------------------------------------------------------- config 2, decode detail
@@ -453,10 +554,51 @@ def lrc_repair(a, r):
         if ev:
             ev[1].record()
 
+    # The reference's own per-stripe call sequence (help_repair's partial, main_repair's partial,
+    # perform_addition: handle_repair.cpp:249,371-376,566) on the same blocks, issued from C++ through the
+    # C ABI (loopback/replay.cpp), as one call per stripe outside any scope, in deferred-batch scopes, and
+    # in scopes with the partials declared scratch (the three calls compose into one region product).
+    rp = replay_lib()
+    sl_h, pl_h = sl.cpu().to(torch.int32).contiguous(), pl.cpu().to(torch.int32).contiguous()
+    n_pat = len(cls_local)
+    fail_h = torch.tensor(cls_local, dtype=torch.int32)
+    surv_h = torch.tensor([azure_local_split(e)[0] for e in cls_local], dtype=torch.int32).contiguous()
+    help_h = torch.tensor([azure_local_split(e)[1][0] for e in cls_local], dtype=torch.int32).contiguous()
+    main_h = torch.tensor([azure_local_split(e)[1][1] for e in cls_local], dtype=torch.int32).contiguous()
+    assert surv_h.shape == (n_pat, 6) and help_h.shape == main_h.shape == (n_pat, 3)
+    part_scratch = torch.empty((sl.numel(), 2, B), dtype=torch.uint8, device="cuda")
+    scope_stripes = 512  # tools/scope_repair.cpp's scope size (profiles/r02/scope_repair/)
+    replay_stats = {}
+
+    def replay(form):
+        def fn(ev=None):
+            if ev:
+                ev[0].record()
+            st = torch.cuda.current_stream().cuda_stream
+            rc = rp.ecg_replay_partial_repair(
+                ec._h, form, scope_stripes, stripes.data_ptr(), stripes.stride(0), stripes.stride(1), B, sl.numel(),
+                sl_h.data_ptr(), pl_h.data_ptr(), fail_h.data_ptr(), 6, surv_h.data_ptr(), 3, help_h.data_ptr(), 3,
+                main_h.data_ptr(), part_scratch.data_ptr(), rebuilt.data_ptr(), rebuilt.stride(0), st)
+            if rc != 0:
+                raise ecg.EcgError(rc, "ecg_replay_partial_repair")
+            if form > 0:
+                replay_stats[form] = ecg.batch_last_stats()
+            ecg.matrix_apply_batch_multi(glob_progs, stripes, rebuilt, prog_of_stripe=pg, stripe_of=sg)
+            if ev:
+                ev[1].record()
+        return fn
+
     idx = torch.arange(S, device="cuda")
     results = {}
-    for name, fn in (("partial_decoding", step_partial), ("partial_decoding_fused_main", step_fused_main),
-                     ("fused", step_fused)):
+    n_local, n_glob = sl.numel(), sg.numel()
+    alg = (n_local * 7 + n_glob * 13) * B  # (survivors + 1) * B per repair
+    forms = (("partial_decoding", step_partial, (n_local * (4 + 4 + 3) + n_glob * 13) * B),
+             ("partial_decoding_fused_main", step_fused_main, (n_local * (4 + 5) + n_glob * 13) * B),
+             ("fused", step_fused, alg),
+             ("reference_sequence_per_call", replay(0), (n_local * (4 + 4 + 3) + n_glob * 13) * B),
+             ("reference_sequence_scope", replay(1), (n_local * (4 + 4 + 3) + n_glob * 13) * B),
+             ("reference_sequence_scope_scratch", replay(2), None))
+    for name, fn, executed in forms:
         rebuilt.zero_()
         for _ in range(a.warmup):
             fn()
@@ -464,19 +606,44 @@ def lrc_repair(a, r):
         assert torch.equal(rebuilt[:, 0], stripes[idx, e_of.long()]), f"{name}: repair mismatch"
         elapsed, evs = timed_loop(r, a.steps, fn)
         t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
-        n_local, n_glob = sl.numel(), sg.numel()
-        alg = (n_local * 7 + n_glob * 13) * B            # (survivors + 1) * B per repair
-        executed = {"fused": alg, "partial_decoding": (n_local * (4 + 4 + 3) + n_glob * 13) * B,
-                    "partial_decoding_fused_main": (n_local * (4 + 5) + n_glob * 13) * B}[name]
-        results[name] = {"repairs_per_s": round(r.world * S * a.steps / elapsed, 1),
-                         "ms_per_batch": round(t * 1e3, 3),
-                         "algorithmic_GBps": round(alg / t / 1e9, 1),
-                         "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
-                         "executed_bytes_per_batch": executed,
-                         "executed_GBps": round(executed / t / 1e9, 1)}
+        res = {"repairs_per_s": round(r.world * S * a.steps / elapsed, 1), "ms_per_batch": round(t * 1e3, 3),
+               "algorithmic_GBps": round(alg / t / 1e9, 1), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+        if name == "reference_sequence_scope_scratch":
+            st = replay_stats[2]  # the last scope's flush: 3 recorded calls per repair, composed to 1
+            res["last_scope_flush"] = st
+            per_scope = n_local - ((n_local - 1) // scope_stripes) * scope_stripes  # the last scope's repairs
+            composed_away = st["recorded"] == 3 * per_scope and st["composed"] == per_scope and st["materialised"] == 0
+            executed = alg if composed_away else None
+            res["partials_composed_away"] = composed_away
+        elif name == "reference_sequence_scope":
+            res["last_scope_flush"] = replay_stats[1]
+        if name.startswith("reference_sequence"):
+            res["issued_from"] = "C++ through the C ABI (loopback/replay.cpp), one ErasureCode call per step per stripe"
+        res["executed_bytes_per_batch"] = executed
+        res["executed_GBps"] = round(executed / t / 1e9, 1) if executed else None
+        results[name] = res
     return {"workload": "Azure-LRC(12,2,2) single-block repair, block s mod 16, 1 MiB", "n_gpus": r.world,
             "stripes_per_gpu": S, "steps": a.steps, "results": results, "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)"}
+
+
+_REPLAY = None
+
+
+def replay_lib():
+    """libecg_replay.so (loopback/replay.cpp, built with libecg): the proxy's per-stripe repair calls
+    issued from C++ through the C ABI."""
+    global _REPLAY
+    if _REPLAY is None:
+        import ctypes
+        path = os.path.join(ROOT, "erasure-codes-prototype_amd", "lib", "libecg_replay.so")
+        ecg.lib()  # libecg first (the replay library links it)
+        L = ctypes.CDLL(path)
+        I, LL, P = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p
+        L.ecg_replay_partial_repair.argtypes = [P, I, I, P, LL, LL, I, I, P, P, P, I, P, I, P, I, P, P, P, LL, P]
+        L.ecg_replay_partial_repair.restype = I
+        _REPLAY = L
+    return _REPLAY
 
 
 def ring_repair_state(r, S, B, chunk):
@@ -663,26 +830,14 @@ def rs4m_waves(a, r):
     """RS(10,4), 4 MiB blocks, 65536 stripes sharded over the ranks; a rank's share (8192 stripes at N=8,
     448 GiB) exceeds HBM, so it is encoded in resident waves of 1024 stripes (56 GiB); each wave's input
     is regenerated on device outside the timed region (tests/test_gpu_parity.py::test_config5_waves runs
-    the same code at a small size against the oracle)."""
+    the same code at a small size against the oracle).  The default workload's line carries the same
+    measurement as its "config5" object (config5 above)."""
     k, m = 10, 4
-    n = k + m
-    B = a.block_size or (4 << 20)
-    total = a.stripes or 65536
-    W = 1024
-    first, last = D.stripe_range(total, r)
+    a.config5_stripes = a.stripes or CONFIG5_STRIPES
+    a.config5_block_size = a.block_size or CONFIG5_BLOCK
     M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
-    D.barrier(r)
-    torch.cuda.synchronize()
-    kernel_s, checks = encode_waves(k, m, M, B, first, last, W)
-    t_max = D.max_over_ranks(kernel_s, r, device="cuda")
-    sums = D.gather_checksums(checks, r, device="cuda")
-    data_bytes = total * k * B
-    per_gpu = (last - first) * n * B / kernel_s / 1e9
-    return {"workload": f"RS(10,4) 4 MiB encode, {total} stripes over {r.world} GPU(s), waves of {W}",
-            "n_gpus": r.world, "aggregate_GiBps": round(data_bytes / t_max / 2 ** 30, 1),
-            "per_gpu_hbm_GBps_rank0": round(per_gpu, 1), "per_gpu_hbm_frac_rank0": round(per_gpu / HBM_PEAK_GBS, 4),
-            "encode_seconds_max": round(t_max, 3), "parity_checksum": f"{D.combine(sums):016x}",
-            "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
+    return {**config5(a, r, M, k, m), "n_gpus": r.world, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
 # ------------------------------------------------------------------------------- host-resident
@@ -761,6 +916,9 @@ def main():
     r = D.from_env()
     if a.gpus is not None and a.gpus != r.world:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={r.world}")
+    stall = os.environ.get("ECG_BENCH_TEST_STALL_RANK")  # fault injection for tests/test_dist_cpu.py only
+    if stall is not None and int(stall) == r.rank:
+        time.sleep(3600)  # this rank never joins: the others must fail within ecg_dist's timeout
     if a.launch_check:
         line = launch_check(a, r)
         if r.rank == 0:

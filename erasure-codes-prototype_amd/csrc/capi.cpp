@@ -60,6 +60,15 @@ int ecg_program_cache_size(void) { return (int)Engine::instance().cache_size(); 
 int ecg_program_sets_retiring(void) { return (int)Engine::instance().retired_pending(); }
 int ecg_host_contexts(void) { return Engine::instance().host_contexts(); }
 
+long long ecg_host_pinned_xfer_threshold(void) {
+    const char* v = getenv("GPU_PINNED_MIN_XFER_SIZE");
+    if (!v || !*v) return 1LL << 20;  // the runtime's default: 1 MiB
+    char* end = nullptr;
+    const long long mib = strtoll(v, &end, 10);
+    if (*end != '\0' || mib < 0 || mib > (1LL << 40)) return -1;
+    return mib << 20;
+}
+
 int ecg_batch_begin(void) { return batch_begin(); }
 int ecg_batch_flush(void) { return batch_flush(); }
 int ecg_batch_end(void) { return batch_end(); }

@@ -217,6 +217,19 @@ void Engine::sweep_retired() {
     std::vector<std::shared_ptr<ProgramSet>> dead;  // freed outside the lock
     {
         std::lock_guard<std::mutex> lk(rmu_);
+        if (retired_.empty()) return;
+        // events are created, recorded and (in the fallback) the device synchronized on THIS engine's
+        // device, whatever the calling thread's current device is
+        int caller_dev = -1;
+        (void)hipGetDevice(&caller_dev);
+        const bool switched = caller_dev != device_ && hipSetDevice(device_) == hipSuccess;
+        struct Restore {
+            bool on;
+            int dev;
+            ~Restore() {
+                if (on) (void)hipSetDevice(dev);
+            }
+        } restore{switched, caller_dev};
         bool sync_all = false;
         for (Retired& r : retired_) {
             if (r.armed || r.ps.use_count() != 1) continue;
@@ -711,7 +724,7 @@ public:
             // expressions reading blocks this call overwrites go out first, together as one op
             if (!uses_.empty()) {
                 fast_.clear();
-                start_collect(&fast_, c.eng, c.B);
+                start_collect(&fast_, c.eng, c.st, c.B);
                 for (const LinearOp& op : *c.ops)
                     for (int id : op.dst_ids) before_write(c.blocks[id]);
                 collect_ = nullptr;
@@ -817,7 +830,7 @@ private:
             }
         }
         real_.clear();
-        start_collect(&real_, c.eng, c.B);
+        start_collect(&real_, c.eng, c.st, c.B);
         for (int p = 0; p < m; p++) {
             uint8_t* d = c.blocks[op.dst_ids[p]];
             if (scratch_->holds(d, c.B)) continue;
@@ -831,10 +844,15 @@ private:
     // While a call's writes are processed, expressions written out because the call overwrites a block
     // they read join the call's own op (`collect_`): one op reads every input before it writes any
     // output, so neither side sees the other's writes (a separate earlier call writing scratch block s
-    // would clobber an s the op itself still reads).
-    void start_collect(RowBuf* rows, Engine* eng, long long B) {
+    // would clobber an s the op itself still reads).  An expression recorded on another stream of the same
+    // device joins too: the flush orders its groups across streams (batch_flush), so the op is ordered
+    // after the other stream's writes to the blocks the expression reads.  Written out on its own stream
+    // instead, it would break the op's read-before-write when the two read each other's blocks (the
+    // sequential interpreter of tests/sanitize/host_fuzz.cpp finds such cycles).
+    void start_collect(RowBuf* rows, Engine* eng, hipStream_t st, long long B) {
         collect_ = rows;
         ceng_ = eng;
+        cst_ = st;
         cB_ = B;
     }
 
@@ -879,7 +897,7 @@ private:
                 eng = slab_[e].eng;
                 st = slab_[e].st;
                 B = slab_[e].B;
-                start_collect(&rows, eng, B);
+                start_collect(&rows, eng, st, B);
             }
             materialise(s);
         }
@@ -979,6 +997,7 @@ private:
     RowBuf* collect_ = nullptr;
     RowBuf real_, fast_, wo_;
     const Engine* ceng_ = nullptr;
+    hipStream_t cst_ = nullptr;
     long long cB_ = 0;
     std::vector<Terms> rows_;
     std::vector<uint8_t*> ins_;
@@ -1053,6 +1072,26 @@ private:
 
 }  // namespace
 
+// Per thread and device: the event batch_flush records behind a group when the next group runs on another
+// stream (created on first use and reused -- a wait takes the event's state at the time of the wait; only
+// threads whose scopes span streams create one, and it is not destroyed at thread exit, when the runtime
+// may already be going down).
+thread_local hipEvent_t t_order_ev[kMaxDevices] = {};
+
+int order_after(hipStream_t st, int dev) {
+    if (dev < 0 || dev >= kMaxDevices) return ECG_EINVAL;
+    if (!t_order_ev[dev] && hipEventCreateWithFlags(&t_order_ev[dev], hipEventDisableTiming) != hipSuccess) {
+        t_order_ev[dev] = nullptr;
+        set_last_error("batch flush: hipEventCreate failed");
+        return ECG_EHIP;
+    }
+    if (hipEventRecord(t_order_ev[dev], st) != hipSuccess) {
+        set_last_error("batch flush: hipEventRecord failed");
+        return ECG_EHIP;
+    }
+    return ECG_OK;
+}
+
 int batch_flush() {
     DeferScope& d = t_defer;
     if (d.q.empty()) return ECG_OK;
@@ -1080,10 +1119,19 @@ int batch_flush() {
     (void)hipGetDevice(&caller_dev);
     cur_dev = caller_dev;
     int rc = ECG_OK;
+    hipStream_t prev_st = nullptr;
     for (size_t g = 0; g < groups.size() && rc == ECG_OK; g++) {
         const std::vector<size_t>& G = groups[g];
         const DeferredCall& c0 = q[G[0]];
         Engine* eng = c0.eng;
+        // Groups run in program order across streams and devices: where the stream changes from one group
+        // to the next, the new stream waits for an event recorded behind the previous group (so a chain
+        // A, B, A orders every group after all earlier ones).  The calls were recorded in one order; a group
+        // on stream B may read blocks an earlier group on A writes, or a scratch combination recorded on A
+        // (compose_scratch joins those to the op that forces them).  One stream: no event at all.
+        const bool switch_st = g > 0 && (c0.st != prev_st || eng->device() != cur_dev);
+        const int ev_dev = cur_dev;  // the previous group's device
+        if (switch_st && (rc = order_after(prev_st, ev_dev)) != ECG_OK) break;
         if (eng->device() != cur_dev) {  // a group launches on the device its calls were recorded on
             if (hipSetDevice(eng->device()) != hipSuccess) {
                 set_last_error("batch flush: hipSetDevice failed");
@@ -1092,6 +1140,12 @@ int batch_flush() {
             }
             cur_dev = eng->device();
         }
+        if (switch_st && hipStreamWaitEvent(c0.st, t_order_ev[ev_dev], 0) != hipSuccess) {
+            set_last_error("batch flush: hipStreamWaitEvent failed");
+            rc = ECG_EHIP;
+            break;
+        }
+        prev_st = c0.st;
         if (G.size() == 1) {
             rc = eng->launch_direct(*c0.ops, c0.blocks.data(), c0.B, c0.st);
             st.launches += (long long)c0.ops->size();

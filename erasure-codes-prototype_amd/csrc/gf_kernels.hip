@@ -26,6 +26,14 @@
 #include "gf_kernels.hpp"
 #include "gf256.hpp"
 
+// gfx950 only: the completion-flag epilogue (gf_done_flag.hpp) encodes its waits for gfx9's vmcnt, which
+// counts stores there; gfx10+ count stores in vscnt, and the flag could then overtake the data.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "gf_kernels.hip is gfx950 (CDNA4) code"
+#endif
+
+#include "gf_done_flag.hpp"
+
 namespace ecg {
 
 namespace {
@@ -150,26 +158,6 @@ template <int MT, int U, bool BIN>
 __device__ __forceinline__ void fold(const uint32_t (&x)[U][4], const ECG_CONST CoefTab* t, uint32_t (&acc)[MT][4]) {
     if constexpr (BIN) fold_binary<MT, U>(x, t, acc);
     else fold_general<MT, U>(x, t, acc);
-}
-
-// Completion flag of a latency-kernel workgroup, for a polling host (vector stores only).  A system-scope
-// release is (1) the issuing wave's own stores complete (s_waitcnt vmcnt(0)), (2) the L2 written back
-// (buffer_wbl2, which covers the whole L2, not one wave's lines) and (3) that write-back complete before
-// the flag store.  So every wave waits for its own stores, the workgroup meets at a barrier, and only
-// lane 0 of wave 0 writes the L2 back and posts the flag: one L2 write-back per workgroup instead of one
-// per wave.  Step (3) is an explicit wait: after the barrier's vmcnt(0) the compiler's wait insertion
-// does not count the write-back as outstanding and drops the wait a release store would carry (seen
-// in the ISA: buffer_wbl2 directly followed by the flag store; a config-1 loopback run then read 3 of
-// 2617 rebuilt blocks stale).
-__device__ __forceinline__ void post_done_flag(const GfLaunch& a) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt / lgkmcnt unconstrained
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: buffer_wbl2
-        __builtin_amdgcn_s_waitcnt(0x0F70);            // the write-back has completed
-        __hip_atomic_store(a.done_flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    }
 }
 
 // Minimum waves per EU the register allocator must allow (r01 sweep, tools/gpu_variants.sh): 8 for the

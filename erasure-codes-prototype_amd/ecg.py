@@ -60,6 +60,7 @@ class RepairPlan:  # include/ec/erasure_code.h:53-58
 # Every symbol include/ecg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free", "ecg_program_cache_size", "ecg_program_sets_retiring", "ecg_host_contexts",
+    "ecg_host_pinned_xfer_threshold",
     "ecg_set_option", "ecg_get_option",
     "ecg_reed_sol_vandermonde_coding_matrix", "ecg_cauchy_good_general_coding_matrix",
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
@@ -151,6 +152,7 @@ def lib():
         "ecg_program_cache_size": ([], I),
         "ecg_program_sets_retiring": ([], I),
         "ecg_host_contexts": ([], I),
+        "ecg_host_pinned_xfer_threshold": ([], LL),
         "ecg_batch_begin": ([], I),
         "ecg_batch_flush": ([], I),
         "ecg_batch_end": ([], I),
@@ -221,6 +223,12 @@ def lib():
         f.restype = res
     _L = L
     return L
+
+
+def host_pinned_xfer_threshold():
+    """ecg_host_pinned_xfer_threshold: bytes above which the HIP runtime pins a pageable copy itself
+    (GPU_PINNED_MIN_XFER_SIZE; default 1 MiB); -1 if the variable is malformed."""
+    return lib().ecg_host_pinned_xfer_threshold()
 
 
 def set_option(option, value):

@@ -16,6 +16,7 @@ the chunks around it.
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 
@@ -43,15 +44,25 @@ def from_env() -> Rank:
 
 _BACKEND = None
 
+# Seconds a rank waits in rendezvous or in any collective before it fails (ECG_DIST_TIMEOUT_S).  A rank
+# that never joins, or an RCCL communicator that never forms, then ends the run with an error instead of
+# holding the node: init_process_group raises once the store rendezvous times out, and a collective that
+# does not complete within it aborts the communicator (torch's watchdog).
+DEFAULT_TIMEOUT_S = 300.0
+
+
+def timeout_s() -> float:
+    return float(os.environ.get("ECG_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+
 
 def init(r: Rank, backend: str = "nccl", device=None) -> None:
     global _BACKEND
     _BACKEND = backend
     if r.distributed and not dist.is_initialized():
+        kw = {"timeout": datetime.timedelta(seconds=timeout_s())}
         if device is not None:
-            dist.init_process_group(backend, device_id=device)
-        else:
-            dist.init_process_group(backend)
+            kw["device_id"] = device
+        dist.init_process_group(backend, **kw)
 
 
 def stripe_range(total: int, r: Rank) -> tuple[int, int]:
@@ -111,6 +122,18 @@ def checksum64(t: torch.Tensor) -> int:
     2^64 (the buffer length must be a multiple of 8)."""
     words = t.reshape(-1).view(torch.int64)
     return int(words.sum().item()) & _MASK64
+
+
+def gather_floats(vals, r: Rank, device="cpu") -> list[list[float]]:
+    """All-gather a short list of floats from every rank: result[q] is rank q's list (same length on
+    every rank).  Per-rank HBM fractions and times for the bench line, after the timed region."""
+    vals = [float(v) for v in vals]
+    if not r.distributed:
+        return [vals]
+    t = torch.tensor(vals, dtype=torch.float64, device=_dev(device))
+    out = [torch.zeros_like(t) for _ in range(r.world)]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.tolist()] for o in out]
 
 
 def combine(checksums) -> int:

@@ -1,0 +1,74 @@
+// libecg_replay.so: the proxy's per-stripe repair call sequence, issued from C++ as the proxy issues it,
+// for bench.py (config 3, `--workload lrc-repair`, form "partial_decoding_scope_scratch").
+//
+// The reference's main/help repair with partial decoding makes, per stripe, three ErasureCode calls
+// (handle_repair.cpp:249,371-376,566): a helper proxy's encode_partial_blocks_for_decoding over its
+// partition's survivors, the main proxy's own encode_partial_blocks_for_decoding, and perform_addition of
+// the two partials into the repaired block.  Driving those calls one by one from Python would measure
+// the interpreter (~10 us per call), not the engine; the proxy is C++.  So this replays the same calls
+// through the C ABI (include/ecg.h, nothing else), on HBM blocks, in one of three forms:
+//   0 direct   every call launched on its own;
+//   1 scope    calls recorded in deferred-batch scopes of `scope_stripes` stripes (ecg_batch_begin/end);
+//   2 scratch  the same scopes with the partial buffers declared scratch (ecg_batch_scratch): the three
+//              calls of a repair compose into one region product and the partials never reach HBM.
+// Not part of libecg (the product); a caller of it, like loopback/.
+#include <vector>
+
+#include "../../include/ecg.h"
+
+extern "C" {
+
+// Repairs launch stripes i < S: stripe st = stripe_of[i] (host int[S]) of the strided batch (block b at
+// base + st * sstride + b * bstride) loses block fail[p], p = pattern_of[i] (host int[S]); pattern p's
+// n_surv survivors surv[p * n_surv ..], of which the helper partition holds help[p * n_help ..] and the
+// main proxy main_[p * n_main ..].  Partials of launch stripe i at partials + (2 i + j) * B (j = 0 helper,
+// 1 main); the repaired block of stripe st at out + st * out_stride.  Asynchronous on `stream`; returns 0 or the first
+// negative ecg_* status.
+int ecg_replay_partial_repair(ecg_ec* ec, int form, int scope_stripes, char* base, long long sstride,
+                              long long bstride, int B, int S, const int* stripe_of, const int* pattern_of,
+                              const int* fail, int n_surv, const int* surv, int n_help, const int* help, int n_main,
+                              const int* main_, char* partials, char* out, long long out_stride, void* stream) {
+    if (!ec || form < 0 || form > 2 || B <= 0 || S < 0 || n_help < 1 || n_main < 1 || n_surv < 1 ||
+        (form > 0 && scope_stripes < 1))
+        return ECG_EINVAL;
+    int rc = ecg_ec_set_memory(ec, ECG_MEM_DEVICE, stream);
+    if (rc) return rc;
+    std::vector<char*> hp(n_help), mp(n_main);
+    auto repair = [&](int i) -> int {
+        const int st = stripe_of[i], p = pattern_of[i];
+        char* blk0 = base + (long long)st * sstride;
+        for (int j = 0; j < n_help; j++) hp[j] = blk0 + (long long)help[p * n_help + j] * bstride;
+        for (int j = 0; j < n_main; j++) mp[j] = blk0 + (long long)main_[p * n_main + j] * bstride;
+        char* pp[2] = {partials + (2LL * i) * B, partials + (2LL * i + 1) * B};
+        const int* sv = surv + (long long)p * n_surv;
+        // help_repair (handle_repair.cpp:566-567), then the main proxy's own partial (:249)
+        int r = ecg_ec_encode_partial_blocks_for_decoding(ec, hp.data(), &pp[0], B, help + p * n_help, n_help, sv,
+                                                          n_surv, fail + p, 1);
+        if (r) return r;
+        r = ecg_ec_encode_partial_blocks_for_decoding(ec, mp.data(), &pp[1], B, main_ + p * n_main, n_main, sv, n_surv,
+                                                      fail + p, 1);
+        if (r) return r;
+        char* o = out + (long long)st * out_stride;
+        return ecg_ec_perform_addition(ec, pp, &o, B, 2, 1);  // handle_repair.cpp:371-376
+    };
+    if (form == 0) {
+        for (int i = 0; i < S; i++)
+            if ((rc = repair(i))) return rc;
+        return 0;
+    }
+    for (int c0 = 0; c0 < S; c0 += scope_stripes) {
+        const int c1 = c0 + scope_stripes < S ? c0 + scope_stripes : S;
+        if ((rc = ecg_batch_begin())) return rc;
+        if (form == 2 && (rc = ecg_batch_scratch(partials + 2LL * c0 * B, (size_t)(c1 - c0) * 2 * B))) {
+            ecg_batch_end();
+            return rc;
+        }
+        for (int i = c0; i < c1 && !rc; i++) rc = repair(i);
+        const int re = ecg_batch_end();
+        if (rc) return rc;
+        if (re) return re;
+    }
+    return 0;
+}
+
+}  // extern "C"

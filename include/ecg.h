@@ -25,6 +25,8 @@
 #ifndef ECG_H
 #define ECG_H
 
+#include <stddef.h> /* size_t (ecg_batch_scratch) */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -50,6 +52,15 @@ int ecg_program_sets_retiring(void);
  * ever in flight at once, not by the number of threads that called (the reference's proxy starts a
  * thread per request, proxy.cpp:416-419). */
 int ecg_host_contexts(void);
+/* The HIP runtime's pinned-transfer threshold for pageable host memory, in bytes, as this process runs
+ * it: GPU_PINNED_MIN_XFER_SIZE (MiB) from the environment, default 1 MiB.  A pageable hipMemcpy of more
+ * than this many bytes is pinned by the runtime for the copy (PCIe DMA rate); one of at most this many is
+ * staged through the runtime's buffer by a CPU memcpy.  Host-tier calls with blocks above 256 KiB copy the
+ * caller's pageable blocks directly, so this decides their speed: an RS(10,4) 1 MiB encode takes ~333 us
+ * at threshold 0 and 478-596 us at the default ("Proxy environment").  The runtime reads
+ * the variable once, when HIP initialises: set it in the process's launch environment.  -1 if the
+ * variable is set but not a non-negative integer (the runtime's own parse then decides). */
+long long ecg_host_pinned_xfer_threshold(void);
 
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
  * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP, ECG_ZEROCOPY_BYTES, ECG_PROGRAM_CACHE, ECG_MAP_GROUP,
@@ -134,9 +145,10 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
  * ONE launch per op unless a data dependence orders them apart (a call reads or writes a block an
  * earlier call writes, or writes one an earlier call reads), so a per-stripe loop that interleaves
  * several plans -- a repair's helper partial, main partial and perform_addition per stripe -- still
- * goes out as one launch per plan.  Groups launch in an order that keeps every such dependence: the
- * outputs are the outputs of the calls run one by one, defined once the flush's work completes on the
- * stream.  A group is a strided launch when its blocks are one strided batch (block b of the c-th call
+ * goes out as one launch per plan.  Groups launch in an order that keeps every such dependence, across
+ * streams too (where consecutive groups run on different streams, the later one's stream waits for an
+ * event behind the earlier group): the outputs are the outputs of the calls run one by one in recorded
+ * order, defined once the flush's work completes on their streams.  A group is a strided launch when its blocks are one strided batch (block b of the c-th call
  * at base + c * stripe_stride + b * block_stride, checked for every pointer), a pointer-table launch
  * otherwise.  Blocks are compared by address: blocks of one scope are identical or disjoint.
  * Host-tier and batched calls made inside the scope (ecg_region_xor_batch and ecg_fill_random

@@ -282,3 +282,43 @@ def test_region_xor_on_coefficient_rows_needs_no_gpu(ecg):
                                              a.nbytes)
         assert rc == 0
         assert np.array_equal(b, want)
+
+
+@pytest.mark.parametrize("setting,want", [(None, 1 << 20), ("0", 0), ("4", 4 << 20), ("", 1 << 20), ("x1", -1),
+                                          ("-2", -1)])
+def test_host_pinned_xfer_threshold(setting, want):
+    """The host-transfer regime a process runs in: GPU_PINNED_MIN_XFER_SIZE as the HIP
+    runtime reads it at initialisation.  Each setting in a fresh process, as a proxy's launch environment
+    would set it; no GPU is touched."""
+    env = {k: v for k, v in os.environ.items() if k != "GPU_PINNED_MIN_XFER_SIZE"}
+    if setting is not None:
+        env["GPU_PINNED_MIN_XFER_SIZE"] = setting
+    code = ("import sys; sys.path.insert(0, 'erasure-codes-prototype_amd'); import ecg; "
+            "print(ecg.host_pinned_xfer_threshold())")
+    out = subprocess.run(["python", "-c", code], capture_output=True, text=True, env=env, cwd=ROOT, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert int(out.stdout.strip().splitlines()[-1]) == want
+
+
+def test_header_compiles_standalone():
+    """include/ecg.h is self-contained C99 and C++ (it needs size_t: a consumer that includes it first, as
+    loopback/replay.cpp does, must not depend on what was included before)."""
+    src = '#include "ecg.h"\nint main(void) { return ECG_OK; }\n'
+    for cc, ext in (("gcc", "c"), ("g++", "cpp")):
+        path = f"/tmp/ecg_hdr_check.{ext}"
+        open(path, "w").write(src)
+        r = subprocess.run([cc, "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-c", path, "-o",
+                            f"/tmp/ecg_hdr_check_{ext}.o"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
+def test_replay_library_refuses_bad_arguments():
+    """bench.py's C++ caller of config 3's per-stripe sequence (loopback/replay.cpp) loads beside libecg and
+    refuses bad arguments before touching a device."""
+    import ctypes
+    import sys
+    sys.argv = sys.argv[:1]
+    import bench
+    L = bench.replay_lib()
+    z = ctypes.c_void_p(0)
+    assert L.ecg_replay_partial_repair(z, 0, 1, z, 0, 0, 16, 1, z, z, z, 6, z, 3, z, 3, z, z, z, 0, z) == -2

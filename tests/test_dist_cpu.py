@@ -51,8 +51,9 @@ def _worker(rank, world, port, total, q):
     t = D.max_over_ranks(float(rank + 1), r, device="cuda")
     n = D.sum_over_ranks(float(last - first), r, device="cuda")
     plan = D.broadcast_ints([7, 1, 255, 0, 42] if rank == 0 else None, r, device="cuda")
+    fl = D.gather_floats([rank, 0.25 * rank, last - first], r, device="cuda")  # bench's per-rank fractions
     D.barrier(r)
-    q.put((rank, first, last, sums, t, n, plan))
+    q.put((rank, first, last, sums, t, n, plan, fl))
     torch.distributed.destroy_process_group()
 
 
@@ -79,6 +80,9 @@ def test_two_rank_sharding_matches_single_process(total):
     assert res[0][5] == res[1][5] == float(total)
     # the coding plan fanned out from rank 0
     assert res[0][6] == res[1][6] == [7, 1, 255, 0, 42]
+    # every rank's float list, in rank order, on every rank
+    want = [[0.0, 0.0, float(res[0][2] - res[0][1])], [1.0, 0.25, float(res[1][2] - res[1][1])]]
+    assert res[0][7] == res[1][7] == want
 
 
 def test_stripe_range_single_and_uneven():
@@ -214,3 +218,55 @@ def test_bench_gpus_must_match_world():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env.update(extra)
+    return env
+
+
+def test_bench_stalled_rank_fails_within_dist_timeout():
+    """A rank that never joins (injected: ECG_BENCH_TEST_STALL_RANK) must not hold the node: the other
+    ranks' init_process_group gives up after ecg_dist's timeout (ECG_DIST_TIMEOUT_S), torch.distributed.run
+    tears the job down, and bench.py exits non-zero -- well before the launcher's own watchdog."""
+    import subprocess
+    import time
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
+                        "--timeout", "200"], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=_bench_env(ECG_BENCH_TEST_STALL_RANK="1", ECG_DIST_TIMEOUT_S="10"))
+    took = time.time() - t0
+    assert p.returncode not in (0, 124), (p.returncode, p.stderr[-2000:])
+    assert took < 150, took
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_launcher_watchdog_kills_stuck_ranks():
+    """The launcher's wall-clock watchdog (--timeout): with the ranks' own timeout far away, a stuck rank
+    is killed with its whole process group and bench.py exits 124 shortly after the limit."""
+    import subprocess
+    import time
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
+                        "--timeout", "15"], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=_bench_env(ECG_BENCH_TEST_STALL_RANK="1", ECG_DIST_TIMEOUT_S="3000"))
+    took = time.time() - t0
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    assert 15 <= took < 60, took
+    assert "terminating them" in p.stderr
+
+
+def test_dist_init_passes_timeout(monkeypatch):
+    """ecg_dist.init hands its timeout to init_process_group (rendezvous and every collective)."""
+    sys.path[:0] = [os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    import datetime
+    import ecg_dist as D
+    seen = {}
+    monkeypatch.setattr(D.dist, "is_initialized", lambda: False)
+    monkeypatch.setattr(D.dist, "init_process_group", lambda backend, **kw: seen.update(kw, backend=backend))
+    monkeypatch.setenv("ECG_DIST_TIMEOUT_S", "42")
+    D.init(D.Rank(0, 2, 0), "nccl", device="cuda:0")
+    assert seen == {"backend": "nccl", "timeout": datetime.timedelta(seconds=42), "device_id": "cuda:0"}
+    D.init(D.Rank(0, 1, 0), "gloo")  # one rank: no process group at all

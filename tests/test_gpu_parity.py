@@ -1178,6 +1178,47 @@ def test_batch_scope_eager_flush(ecg, torch_cuda, with_scratch):
     assert stats["recorded"] == (2 * S if with_scratch else (2 * S) % 1024), stats
 
 
+def test_batch_scope_orders_streams(ecg, torch_cuda):
+    """Calls recorded on two streams in one scope keep their recorded order: the flush makes a
+    group wait for an event behind the previous group where the stream changes.  Stream A encodes a large
+    batch; stream B then adds each stripe's first two parities (reads A's output); and a helper partial
+    recorded on A into declared scratch is consumed by a perform_addition recorded on B (the composed op
+    runs on B and must see A's encode).  Without the ordering, B's kernels race A's."""
+    torch = torch_cuda
+    k, m, S, B = 10, 4, 256, 1 << 20
+    n = k + m
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    st = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, 0x0D3D)
+    st[:, k:] = 0
+    out = torch.zeros((S, 2, B), dtype=torch.uint8, device="cuda")
+    scratch = torch.empty((S, B), dtype=torch.uint8, device="cuda")
+    ref = st.clone()
+    ecg.encode_batch(k, m, M, ref[:, :k], ref[:, k:])
+    want0 = ref[:, k] ^ ref[:, k + 1]
+    want1 = ref[:, k + 2] ^ ref[:, k + 3] ^ ref[:, 0]
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
+    for _ in range(2):
+        out.zero_()
+        st[:, k:] = 0
+        torch.cuda.synchronize()
+        with ecg.batch() as scope:
+            scope.scratch(scratch)
+            for s in range(S):
+                ec.encode([st[s, j] for j in range(k)], [st[s, k + i] for i in range(m)], B, stream=sa.cuda_stream)
+            for s in range(S):
+                ec.perform_addition([st[s, k], st[s, k + 1]], [out[s, 0]], B, 2, 1, stream=sb.cuda_stream)
+            for s in range(S):  # scratch partial on A, consumed on B
+                ec.perform_addition([st[s, k + 2], st[s, k + 3]], [scratch[s]], B, 2, 1, stream=sa.cuda_stream)
+                ec.perform_addition([scratch[s], st[s, 0]], [out[s, 1]], B, 2, 1, stream=sb.cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(st, ref)
+        assert torch.equal(out[:, 0], want0), "stream B read parities before stream A wrote them"
+        assert torch.equal(out[:, 1], want1), "composed op on stream B did not see stream A's encode"
+
+
 def test_batch_scope_hazards_split_runs(ecg, torch_cuda):
     """Calls with the same plan that depend on each other (a chain of galois_region_xor-like additions
     through perform_addition) must keep their sequential meaning inside a scope."""

@@ -186,8 +186,14 @@ def test_eviction_does_not_stall_other_streams(ecg, oracle):
         control = timed_calls()  # the same launches, no eviction
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 2)
         evicting = timed_calls()  # every call builds its program again and evicts
-        assert evicting < control + 0.05, (f"evicting calls {evicting:.3f} s vs control {control:.3f} s "
-                                           f"({reps} x {one * 1e3:.2f} ms queued on the other stream)")
+        # A device-wide synchronize on the eviction path would make the evicting calls wait for the whole
+        # queue (~0.4 s); scheduling noise on a shared GPU is far below that.  So the bound is a quarter of
+        # the queued time, not a fixed few ms; the timings are printed as the metric.
+        queued = reps * one
+        print(f"eviction: {evicting * 1e3:.1f} ms vs control {control * 1e3:.1f} ms, {queued * 1e3:.0f} ms queued")
+        assert evicting < control + max(0.05, 0.25 * queued), (
+            f"evicting calls {evicting:.3f} s vs control {control:.3f} s ({reps} x {one * 1e3:.2f} ms queued "
+            f"on the other stream)")
         host = blocks.cpu().numpy()
         for Mi, out in zip(mats, outs):
             want = [np.zeros(Bs, np.uint8) for _ in range(2)]

@@ -24,6 +24,13 @@ c1 = D.combine(int(x, 16) for x in rs1["parity_checksums"])
 c2 = D.combine(int(x, 16) for x in rs2["parity_checksums"])
 print(f"rs-encode-decode: N=1 512 stripes {c1:016x}; N=2 x 256 {c2:016x}; n_gpus={rs2['n_gpus']}")
 ok &= c1 == c2 and rs2["n_gpus"] == 2 and len(rs2["parity_checksums"]) == 2
+for nm, x in (("N=1", rs1), ("N=2", rs2)):  # the default line's config5 object (full 65536 x 4 MiB batch)
+    c5 = x["config5"]
+    print(f"config5 {nm}: {c5['parity_checksum']} (N=1 reference {c5['parity_checksum_n1']}), "
+          f"stripes per rank {c5['stripes_per_rank']}, hbm_frac per rank {c5['hbm_frac_per_rank']}")
+    ok &= c5["checksum_equals_n1"] is True and len(c5["hbm_frac_per_rank"]) == x["n_gpus"]
+print("per_rank", rs2["per_rank"])
+ok &= len(rs2["per_rank"]["encode_frac"]) == 2 and len(rs2["per_rank"]["decode_frac"]) == 2
 spawn = f"{d}/rs_n2_selfspawn.log"
 if os.path.exists(spawn):  # bench.py --gpus 2 started its own ranks (torch.distributed.run child)
     rs2s = line(spawn)
