@@ -60,6 +60,10 @@ int ecg_program_cache_size(void) { return (int)Engine::instance().cache_size(); 
 int ecg_program_sets_retiring(void) { return (int)Engine::instance().retired_pending(); }
 int ecg_host_contexts(void) { return Engine::instance().host_contexts(); }
 
+int ecg_call_worker_stats(long long* calls, long long* launches, long long* relaunches, int* disabled) {
+    return call_worker_stats(calls, launches, relaunches, disabled);
+}
+
 long long ecg_host_pinned_xfer_threshold(void) {
     const char* v = getenv("GPU_PINNED_MIN_XFER_SIZE");
     if (!v || !*v) return 1LL << 20;  // the runtime's default: 1 MiB

@@ -1330,6 +1330,209 @@ static int wait_flags(HostCtx& c, int n, unsigned seq, hipStream_t st) {
     return ECG_OK;
 }
 
+namespace {
+
+// Resident call worker of a device (ECG_OPT_CALL_WORKER > 0; gf_kernels.hpp WorkerArgs).
+// A small synchronous host-tier call normally pays a kernel launch (~4 us of an ~11 us RS(6,4) 1 KiB call);
+// with the worker, a resident kernel polls a descriptor ring in pinned host memory and the call only
+// writes its descriptor (tools/persist_probe.hip: 11.4 -> 4.9 us).  One call at a time goes through it
+// (try_lock): concurrent callers take the launch path, so concurrency is never serialised behind it.
+// The worker runs on a HIGH-PRIORITY stream: HIP maps streams onto a few hardware queues, and a kernel
+// that stays resident on a queue shared with another stream holds that stream's work behind it until it
+// exits (measured: 28 ms for one of 8 normal streams, none with the worker on a high-priority stream;
+// profiles/r03/persist/queue_interference.log).  A process that issues its own work on high-priority
+// streams shares that queue -- hence the option is off by default.  The worker exits by itself after the
+// option's idle time without a call (and after 50 ms in all), and at process exit.
+struct CallWorker {
+    static constexpr double kLifeMs = 50.0;
+    std::mutex mu;
+    bool ready = false, broken = false, running = false;
+    int device = 0;
+    hipStream_t st = nullptr;
+    uint8_t* host = nullptr;  // pinned, mapped: ring [0, 1024), flags [1024, 1280), stop @2048, exit_info @2112
+    uint8_t* host_dev = nullptr;
+    uint8_t* dmem = nullptr;  // device: mailbox [0, 1024), mailbox seqs + exit word @1024
+    unsigned seq = 0, gen = 0;
+    int W = 0;
+    unsigned long long ticks_per_us = 100;
+    long long idle_us = 0, gen_idle_us = 0;  // the option now / the running generation's idle limit
+    long long calls = 0, launches = 0, relaunches = 0;
+
+    WorkerDesc* ring() { return (WorkerDesc*)host; }
+    unsigned* flags() { return (unsigned*)(host + 1024); }
+    volatile unsigned* stopw() { return (volatile unsigned*)(host + 2048); }
+    unsigned* exit_info() { return (unsigned*)(host + 2112); }
+
+    bool init(int dev) {
+        device = dev;
+        int lo = 0, hi = 0, khz = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return false;
+        if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi) != hipSuccess) return false;
+        if (hipHostMalloc((void**)&host, 4096, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return false;
+        if (hipHostGetDevicePointer((void**)&host_dev, host, 0) != hipSuccess) return false;
+        memset(host, 0, 4096);
+        if (hipMalloc((void**)&dmem, 2048) != hipSuccess) return false;
+        if (hipMemsetAsync(dmem, 0, 2048, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return false;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) return false;
+        ticks_per_us = (unsigned long long)khz / 1000ULL;
+        if (ticks_per_us == 0) ticks_per_us = 1;
+        ready = true;
+        return true;
+    }
+    // every workgroup of the current generation has exited (it writes `gen` as it leaves)
+    bool gone() {
+        if (!running) return true;
+        for (int w = 0; w < W; w++)
+            if (__atomic_load_n(&exit_info()[w], __ATOMIC_ACQUIRE) != gen) return false;
+        running = false;
+        return true;
+    }
+    int launch(int workgroups, unsigned start) {
+        WorkerArgs a;
+        memset(&a, 0, sizeof a);
+        if (++gen == 0) ++gen;
+        a.ring = (const WorkerDesc*)host_dev;
+        a.flags = (unsigned*)(host_dev + 1024);
+        a.stop = (const unsigned*)(host_dev + 2048);
+        a.mbox = (WorkerDesc*)dmem;
+        a.mbseq = (unsigned*)(dmem + 1024);
+        a.exit_info = (unsigned*)(host_dev + 2112);
+        a.start_seq = start;
+        a.gen = gen;
+        a.max_polls = 1u << 24;
+        a.idle_ticks = (unsigned long long)idle_us * ticks_per_us;
+        a.life_ticks = (unsigned long long)(kLifeMs * 1000.0) * ticks_per_us;
+        *stopw() = 0;
+        const hipError_t e = launch_call_worker(a, workgroups, st);
+        if (e != hipSuccess) {
+            set_last_error(std::string("call worker launch: ") + hipGetErrorString(e));
+            return ECG_EHIP;
+        }
+        W = workgroups;
+        gen_idle_us = idle_us;
+        running = true;
+        launches++;
+        return ECG_OK;
+    }
+    // stop the running generation and wait until it is gone (bounded: it exits at its next poll)
+    int stop() {
+        if (!running) return ECG_OK;
+        *stopw() = 1;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!gone()) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                if (hipStreamSynchronize(st) != hipSuccess) return ECG_EHIP;
+                running = false;
+                break;
+            }
+            __builtin_ia32_pause();
+        }
+        *stopw() = 0;
+        return ECG_OK;
+    }
+    bool done(unsigned slot, unsigned s) {
+        const unsigned* f = flags() + slot * kWorkerMaxWG;
+        for (int w = 0; w < W; w++)
+            if (__atomic_load_n(&f[w], __ATOMIC_ACQUIRE) != s) return false;
+        return true;
+    }
+    // One call: 0 = done, 1 = not taken (use the launch path), < 0 = error.
+    int call(int dev_id, const ProgramSet& ps, const LinearOp& op, uint8_t* const* dev, long long B) {
+        if (broken) return 1;
+        if (!ready && !init(dev_id)) {
+            broken = true;
+            return 1;
+        }
+        idle_us = get_option(ECG_OPT_CALL_WORKER);
+        const int need = (int)std::max(1LL, ((B >> 2) + kLatThreads - 1) / kLatThreads);
+        if (need > kWorkerMaxWG) return 1;
+        unsigned s = ++seq;
+        if (s == 0) s = ++seq;
+        const unsigned slot = s % kWorkerSlots;
+        // payload, then the four sequence numbers (x86 stores become visible in program order)
+        WorkerDesc& d = ring()[slot];
+        unsigned pay[60] = {};
+        pay[WF_K] = (unsigned)op.k_in();
+        pay[WF_M] = (unsigned)op.m_out();
+        pay[WF_B] = (unsigned)B;
+        pay[WF_BINARY] = ps.binary ? 1u : 0u;
+        auto put64 = [&](int q, const void* p) {
+            pay[q] = (unsigned)(uintptr_t)p;
+            pay[q + 1] = (unsigned)((uintptr_t)p >> 32);
+        };
+        put64(WF_TABS, ps.d_tabs);
+        for (int j = 0; j < op.k_in(); j++) put64(WF_IN + 2 * j, dev[op.src_ids[j]]);
+        for (int p = 0; p < op.m_out(); p++) put64(WF_OUT + 2 * p, dev[op.dst_ids[p]]);
+        for (int q = 0; q < 60; q++) d.w[worker_pos(q)] = pay[q];
+        std::atomic_thread_fence(std::memory_order_release);
+        for (int l = 0; l < 4; l++) __atomic_store_n(&d.w[16 * l], s, __ATOMIC_RELEASE);
+        // a generation too narrow for this call, or started under another idle limit, makes way for a new one
+        if (!gone() && (W < need || gen_idle_us != idle_us) && stop() != ECG_OK) return ECG_EHIP;
+        if (!running && launch(std::max(need, 1), s) != ECG_OK) {
+            broken = true;
+            return 1;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        auto next_check = t0 + std::chrono::microseconds(20);
+        while (!done(slot, s)) {
+            const auto t = std::chrono::steady_clock::now();
+            if (t > next_check) {
+                next_check = t + std::chrono::microseconds(20);
+                if (gone() && !done(slot, s)) {  // the generation left before taking the call: a new one takes it
+                    relaunches++;
+                    if (launch(std::max(need, W), s) != ECG_OK) {
+                        broken = true;
+                        return 1;
+                    }
+                }
+            }
+            if (t - t0 > std::chrono::milliseconds(100)) {
+                // not expected: take the launch path for this call and stop using the worker
+                (void)stop();
+                (void)hipStreamSynchronize(st);
+                broken = true;
+                set_last_error("call worker: a call did not complete within 100 ms; worker disabled");
+                return done(slot, s) ? 0 : 1;
+            }
+            if (t - t0 > std::chrono::microseconds(200)) std::this_thread::yield();
+            else __builtin_ia32_pause();
+        }
+        calls++;
+        return 0;
+    }
+};
+
+CallWorker g_worker[kMaxDevices];
+
+// At process exit: tell running workers to stop (a store to pinned host memory) and wait briefly for them
+// to leave -- no HIP call, the runtime may already be going down.  They would leave by themselves within
+// their idle time anyway.
+struct WorkerReaper {
+    ~WorkerReaper() {
+        for (CallWorker& w : g_worker) {
+            if (!w.ready || !w.running) continue;
+            *w.stopw() = 1;
+            const auto t0 = std::chrono::steady_clock::now();
+            while (!w.gone() && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20)) __builtin_ia32_pause();
+        }
+    }
+} g_worker_reaper;
+
+}  // namespace
+
+int call_worker_stats(long long* calls, long long* launches, long long* relaunches, int* disabled) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDevices) return ECG_EINVAL;
+    CallWorker& w = g_worker[dev];
+    std::lock_guard<std::mutex> lk(w.mu);
+    if (calls) *calls = w.calls;
+    if (launches) *launches = w.launches;
+    if (relaunches) *relaunches = w.relaunches;
+    if (disabled) *disabled = w.broken ? 1 : 0;
+    return ECG_OK;
+}
+
 // Host-buffer tier (the reference's per-stripe calls on host memory).  Device slots are assigned to the
 // blocks that must be uploaded first (read before any op writes them), then to the rest, so the
 // inputs form one contiguous range.  Small calls (the proxy's 1 KiB - 64 KiB blocks) gather those
@@ -1411,6 +1614,30 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         // host polls the flags instead of synchronizing the stream -- the runtime's completion round trip is
         // ~4 us of a ~14 us call (tools/small_call.cpp, profiles/r02/small_call/).  Only for launches whose
         // vector path covers every byte and that fit the flag page; anything else synchronizes as before.
+        // the resident call worker, when enabled: one op of at most 16 inputs and 4 outputs, blocks of at
+        // most 16 KiB in 4-byte lanes, tables already resident; anything else takes the launch path below
+        if (ops.size() == 1 && B > 0 && (B % 4) == 0 && get_option(ECG_OPT_CALL_WORKER) > 0) {
+            const LinearOp& op = ops[0];
+            if (op.k_in() >= 1 && op.k_in() <= kWorkerMaxSrc && op.m_out() >= 1 && op.m_out() <= kWorkerMaxRows) {
+                CallWorker& wk = g_worker[device_];
+                std::unique_lock<std::mutex> lk(wk.mu, std::try_to_lock);
+                if (lk.owns_lock()) {
+                    int status = ECG_OK;
+                    std::shared_ptr<ProgramSet> ps = program_set(&op, 1, &status, st);
+                    if (!ps) return status;
+                    if (ps->ready.load(std::memory_order_acquire) || hipEventQuery(ps->ready_ev) == hipSuccess) {
+                        (void)ps->ensure_ready(st);  // marks the set ready (its upload has completed)
+                        const int rc = wk.call(device_, *ps, op, dev.data(), B);
+                        if (rc < 0) return rc;
+                        if (rc == 0) {
+                            for (int id = 0; id < nblocks; id++)
+                                if (written[id]) memcpy(blocks[id], c.pinned + (size_t)slot[id] * pitch, (size_t)B);
+                            return lease.done();
+                        }
+                    }
+                }
+            }
+        }
         bool flagged = (B % 16) == 0 && flags_ready(c);
         for (const LinearOp& op : ops)
             flagged &= op.k_in() > 0 && op.k_in() <= kInlineSrc && op.m_out() <= kInlineDst;

@@ -330,6 +330,10 @@ std::vector<std::vector<size_t>> schedule_groups(size_t n, Key key, Reads reads,
     return groups;
 }
 
+// Resident call worker of the calling thread's device (ECG_OPT_CALL_WORKER): calls, launches, relaunches,
+// disabled after a failure.
+int call_worker_stats(long long* calls, long long* launches, long long* relaunches, int* disabled);
+
 // Last HIP error seen by this thread (for diagnostics through the C ABI).
 const char* last_error_string();
 void set_last_error(const std::string& s);

@@ -17,7 +17,8 @@
 
 namespace ecg {
 
-__device__ __forceinline__ void post_done_flag(const GfLaunch& a) {
+// flag = this workgroup's slot (every thread of the workgroup calls this)
+__device__ __forceinline__ void post_done_flag(unsigned* flag, unsigned seq) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt / lgkmcnt unconstrained
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -25,9 +26,12 @@ __device__ __forceinline__ void post_done_flag(const GfLaunch& a) {
 #ifndef ECG_TEST_DROP_FLAG_WAIT
         __builtin_amdgcn_s_waitcnt(0x0F70);            // the write-back has completed
 #endif
-        __hip_atomic_store(a.done_flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+__device__ __forceinline__ void post_done_flag(const GfLaunch& a) {
+    post_done_flag(a.done_flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq);
 }
 
 }  // namespace ecg

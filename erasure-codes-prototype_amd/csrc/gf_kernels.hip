@@ -287,9 +287,8 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
 // inputs (u >= k) re-read input 0 with table 0 and are masked out of the sum.
 // kLatThreads dword columns per workgroup; grid.x = ceil((B / 4) / kLatThreads), grid.y = row tiles.
 template <int MT, bool BIN, int KB>
-__device__ __forceinline__ void lat_fold(const GfLaunch& a, const ECG_CONST CoefTab* T, const uint32_t (&x)[KB],
+__device__ __forceinline__ void lat_fold(const int k, const ECG_CONST CoefTab* T, const uint32_t (&x)[KB],
                                          uint32_t (&acc)[MT]) {
-    const int k = a.k;
 #pragma unroll
     for (int p = 0; p < MT; ++p) acc[p] = 0u;
 #pragma unroll
@@ -333,7 +332,7 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLa
         }
         __builtin_amdgcn_sched_barrier(0);
         uint32_t acc[MT];
-        lat_fold<MT, BIN, KB>(a, T, x, acc);
+        lat_fold<MT, BIN, KB>(a.k, T, x, acc);
         if (live) {
 #pragma unroll
             for (int p = 0; p < MT; ++p)
@@ -346,12 +345,138 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLa
         for (int u = 0; u < KB; ++u)
             x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(a.isrc[u < k ? u : 0] + off));
         uint32_t acc[MT];
-        lat_fold<MT, BIN, KB>(a, T, x, acc);
+        lat_fold<MT, BIN, KB>(a.k, T, x, acc);
 #pragma unroll
         for (int p = 0; p < MT; ++p)
             if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(a.idst[row0 + p] + off));
     }
     if (a.done_flags) post_done_flag(a);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Resident call worker (gf_kernels.hpp WorkerArgs; engine.cpp CallWorker).  Workgroup 0 (the leader)
+// polls the descriptor ring in pinned host memory and the host's stop word -- one PCIe round trip per
+// poll -- and republishes each descriptor it takes in a device-memory mailbox, which the other
+// workgroups poll (L2), so an idle worker reads 256 bytes over the link per poll, not 256 per workgroup.
+// Each call then runs like gf_lat_dword_kernel (4 bytes per lane, every input load in flight at once,
+// KB-bucket straight-line fold) over the workgroup's dword columns, and every workgroup posts its flag
+// with the same release sequence (gf_done_flag.hpp); it takes each call's inputs behind a system-scope
+// acquire, as a fresh launch would.  Bounded: a workgroup exits on the stop word, on
+// the leader's exit word, after idle_ticks without a call (followers wait twice as long), after
+// life_ticks in total or after max_polls polls -- whichever comes first -- and writes `gen` into its
+// exit_info slot as it goes, so the host knows when the whole generation is gone.
+
+__device__ __forceinline__ unsigned long long wk_ptr(const unsigned* d, int q) {
+    return ((unsigned long long)d[worker_pos(q + 1)] << 32) | d[worker_pos(q)];
+}
+
+template <int MT, bool BIN, int KB>
+__device__ __forceinline__ void worker_call(const unsigned* d) {
+    const int k = (int)d[worker_pos(WF_K)];
+    const int m = (int)d[worker_pos(WF_M)];
+    const long long ndw = (long long)d[worker_pos(WF_B)] >> 2;
+    const ECG_CONST CoefTab* T = (const ECG_CONST CoefTab*)(uintptr_t)wk_ptr(d, WF_TABS);
+    const uint8_t* in[KB];
+#pragma unroll
+    for (int u = 0; u < KB; u++) in[u] = (const uint8_t*)(uintptr_t)wk_ptr(d, WF_IN + 2 * (u < k ? u : 0));
+    uint8_t* out[MT];
+#pragma unroll
+    for (int p = 0; p < MT; p++) out[p] = (uint8_t*)(uintptr_t)wk_ptr(d, WF_OUT + 2 * (p < m ? p : 0));
+    for (long long c = (long long)blockIdx.x * kLatThreads + threadIdx.x; c < ndw; c += (long long)gridDim.x * kLatThreads) {
+        uint32_t x[KB];
+#pragma unroll
+        for (int u = 0; u < KB; u++) x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(in[u]) + c);
+        uint32_t acc[MT];
+        lat_fold<MT, BIN, KB>(k, T, x, acc);
+#pragma unroll
+        for (int p = 0; p < MT; p++)
+            if (p < m) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(out[p]) + c);
+    }
+}
+
+template <int MT, bool BIN>
+__device__ __forceinline__ void worker_call_k(const unsigned* d) {
+    const unsigned k = d[worker_pos(WF_K)];
+    if (k <= 4) worker_call<MT, BIN, 4>(d);
+    else if (k <= 6) worker_call<MT, BIN, 6>(d);
+    else if (k <= 8) worker_call<MT, BIN, 8>(d);
+    else if (k <= 10) worker_call<MT, BIN, 10>(d);
+    else if (k <= 12) worker_call<MT, BIN, 12>(d);
+    else worker_call<MT, BIN, 16>(d);
+}
+
+template <bool BIN>
+__device__ __forceinline__ void worker_call_m(const unsigned* d) {
+    switch (d[worker_pos(WF_M)]) {
+        case 1: worker_call_k<1, BIN>(d); break;
+        case 2: worker_call_k<2, BIN>(d); break;
+        case 3: worker_call_k<3, BIN>(d); break;
+        default: worker_call_k<4, BIN>(d); break;
+    }
+}
+
+__global__ void __launch_bounds__(kLatThreads, 1) gf_call_worker_kernel(const WorkerArgs a) {
+    __shared__ unsigned d[64];
+    __shared__ unsigned go;
+    const int tid = threadIdx.x;
+    const bool leader = blockIdx.x == 0;
+    unsigned next = a.start_seq;
+    const unsigned long long t0 = wall_clock64();
+    unsigned long long last = t0;
+    const unsigned long long my_idle = leader ? a.idle_ticks : 2 * a.idle_ticks;
+    for (unsigned polls = 0; polls < a.max_polls; polls++) {
+        const unsigned slot = next % (unsigned)kWorkerSlots;
+        if (leader) {
+            if (tid < 64) {  // wave 0: the descriptor and the stop word in one round trip
+                const unsigned v = __hip_atomic_load(&a.ring[slot].w[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const unsigned stop = __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                d[tid] = v;
+                if (tid == 0) go = stop ? 2u : 0u;
+            }
+            __syncthreads();
+            if (tid == 0 && go == 0 && d[0] == next && d[16] == next && d[32] == next && d[48] == next) go = 1;
+            __syncthreads();
+            if (go == 1 && gridDim.x > 1 && tid < 64) {  // republish for the followers: payload, then seq
+                __hip_atomic_store(&a.mbox[slot].w[tid], d[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tid == 0) __hip_atomic_store(&a.mbseq[slot], next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            if (tid == 0) {
+                const unsigned sq = __hip_atomic_load(&a.mbseq[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned ex = __hip_atomic_load(&a.mbseq[kWorkerSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                go = sq == next ? 1u : ex == a.gen ? 2u : 0u;
+            }
+            __syncthreads();
+            if (go == 1 && tid < 64)
+                d[tid] = __hip_atomic_load(&a.mbox[slot].w[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+        }
+        const unsigned g = go;
+        if (g == 2) break;
+        if (g == 0) {
+            const unsigned long long t = wall_clock64();
+            if (t - last > my_idle || t - t0 > a.life_ticks) break;
+            __syncthreads();  // d / go are rewritten by the next poll
+            continue;
+        }
+        // Acquire at system scope before the call's inputs are read: the staging area is reused call after
+        // call, and a resident kernel -- unlike a fresh launch, whose start invalidates the caches -- would
+        // otherwise read lines of an earlier call's inputs still held in the CU / L2 caches (every call
+        // after the first one read stale data without this, tests/test_gpu_worker.py).
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (d[worker_pos(WF_BINARY)]) worker_call_m<true>(d);
+        else worker_call_m<false>(d);
+        post_done_flag(a.flags + (size_t)slot * kWorkerMaxWG + blockIdx.x, next);
+        next++;
+        last = wall_clock64();
+        __syncthreads();
+    }
+    // No release needed on the way out: nothing follows these stores, and every output of the workgroup
+    // went out behind its call's flag.
+    if (tid == 0) {
+        if (leader) __hip_atomic_store(&a.mbseq[kWorkerSlots], a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.exit_info + blockIdx.x, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Byte path: bytes [off0, B) (tails, unaligned pointers).  cols_per_wg = bytes per workgroup.
@@ -428,6 +553,7 @@ void init_options() {
     g_opt[ECG_OPT_PROGRAM_CACHE].store(env("ECG_PROGRAM_CACHE", 4096));
     g_opt[ECG_OPT_MAP_GROUP].store(env("ECG_MAP_GROUP", 1));
     g_opt[ECG_OPT_LAT_DWORD_BYTES].store(env("ECG_LAT_DWORD_BYTES", 1 << 20));
+    g_opt[ECG_OPT_CALL_WORKER].store(env("ECG_CALL_WORKER", 0));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -546,6 +672,7 @@ int set_option(int opt, long long value) {
     if (opt == ECG_OPT_PROGRAM_CACHE && value < 2) return -1;
     if (opt == ECG_OPT_MAP_GROUP && (value < 1 || value > (1 << 20))) return -1;
     if (opt == ECG_OPT_LAT_DWORD_BYTES && value < 0) return -1;
+    if (opt == ECG_OPT_CALL_WORKER && (value < 0 || value > 1000000)) return -1;  // idle limit <= 1 s
     g_opt[opt].store(value);
     return 0;
 }
@@ -641,6 +768,12 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_call_worker(const WorkerArgs& a, int workgroups, hipStream_t st) {
+    if (workgroups < 1 || workgroups > kWorkerMaxWG) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gf_call_worker_kernel, dim3((unsigned)workgroups), dim3(kLatThreads), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill_splitmix(void* dst, long long nbytes, unsigned long long seed,

@@ -79,6 +79,40 @@ struct GfLaunch {
     unsigned done_seq;
 };
 
+// ---- resident call worker (ECG_OPT_CALL_WORKER) ----
+// Small synchronous host-tier calls can skip the launch: a resident kernel on its own high-priority
+// stream polls a ring of descriptors in pinned host memory and runs each call as the latency kernel
+// would.  A descriptor is four 64-byte lines; dword 0 of every line is the call's sequence number and the
+// host writes it last, so the worker takes a descriptor only when all four lines carry the number it
+// waits for.  The other 60 dwords hold the payload in order (worker_pos maps payload index -> dword).
+constexpr int kWorkerSlots = 4;     // ring slots (one call in flight: the engine serialises the worker)
+constexpr int kWorkerMaxWG = 16;    // workgroups of a worker: blocks up to 16 KiB in one pass of 4-byte lanes
+constexpr int kWorkerMaxSrc = 16;   // inputs per call
+constexpr int kWorkerMaxRows = 4;   // outputs per call (one row tile)
+struct alignas(256) WorkerDesc {
+    unsigned w[64];
+};
+enum WorkerField : int {  // payload indices
+    WF_K = 0, WF_M = 1, WF_B = 2, WF_BINARY = 3, WF_TABS = 4,  // tabs: 2 dwords
+    WF_IN = 8,                                                // 16 input pointers, 2 dwords each
+    WF_OUT = WF_IN + 2 * kWorkerMaxSrc,                       // 4 output pointers
+    WF_END = WF_OUT + 2 * kWorkerMaxRows
+};
+static_assert(WF_END <= 60, "worker payload fits 60 dwords");
+__host__ __device__ constexpr int worker_pos(int q) { return q + 1 + q / 15; }
+
+struct WorkerArgs {
+    const WorkerDesc* ring;  // [kWorkerSlots], pinned host (device view)
+    unsigned* flags;         // [kWorkerSlots][kWorkerMaxWG], pinned host: flag of (call, workgroup) = seq
+    const unsigned* stop;    // pinned host: nonzero = exit at the next poll
+    WorkerDesc* mbox;        // [kWorkerSlots] device: the leader's copy of a descriptor for the others
+    unsigned* mbseq;         // [kWorkerSlots + 1] device: sequence number per mailbox slot, then the exit word
+    unsigned* exit_info;     // [kWorkerMaxWG] pinned host: `gen` once the workgroup has exited
+    unsigned start_seq, gen, max_polls;
+    unsigned long long idle_ticks, life_ticks;  // wall-clock ticks (hipDeviceAttributeWallClockRate, kHz)
+};
+hipError_t launch_call_worker(const WorkerArgs& a, int workgroups, hipStream_t stream);
+
 // Runtime tuning options (ecg_set_option): see ECG_OPT_* in include/ecg.h.
 long long get_option(int opt);
 int set_option(int opt, long long value);

@@ -39,7 +39,8 @@ ECG_OPT_ZEROCOPY_BYTES = 3
 ECG_OPT_PROGRAM_CACHE = 4
 ECG_OPT_MAP_GROUP = 5
 ECG_OPT_LAT_DWORD_BYTES = 6
-ECG_OPT_COUNT = 7
+ECG_OPT_CALL_WORKER = 7
+ECG_OPT_COUNT = 8
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 
@@ -60,7 +61,7 @@ class RepairPlan:  # include/ec/erasure_code.h:53-58
 # Every symbol include/ecg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free", "ecg_program_cache_size", "ecg_program_sets_retiring", "ecg_host_contexts",
-    "ecg_host_pinned_xfer_threshold",
+    "ecg_host_pinned_xfer_threshold", "ecg_call_worker_stats",
     "ecg_set_option", "ecg_get_option",
     "ecg_reed_sol_vandermonde_coding_matrix", "ecg_cauchy_good_general_coding_matrix",
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
@@ -153,6 +154,7 @@ def lib():
         "ecg_program_sets_retiring": ([], I),
         "ecg_host_contexts": ([], I),
         "ecg_host_pinned_xfer_threshold": ([], LL),
+        "ecg_call_worker_stats": ([ctypes.POINTER(LL)] * 3 + [ctypes.POINTER(I)], I),
         "ecg_batch_begin": ([], I),
         "ecg_batch_flush": ([], I),
         "ecg_batch_end": ([], I),
@@ -229,6 +231,14 @@ def host_pinned_xfer_threshold():
     """ecg_host_pinned_xfer_threshold: bytes above which the HIP runtime pins a pageable copy itself
     (GPU_PINNED_MIN_XFER_SIZE; default 1 MiB); -1 if the variable is malformed."""
     return lib().ecg_host_pinned_xfer_threshold()
+
+
+def call_worker_stats():
+    """ecg_call_worker_stats of the current device: {calls, launches, relaunches, disabled}."""
+    v = [ctypes.c_longlong(0) for _ in range(3)]
+    dis = ctypes.c_int(0)
+    _check(lib().ecg_call_worker_stats(*[ctypes.byref(x) for x in v], ctypes.byref(dis)), "call_worker_stats")
+    return {"calls": v[0].value, "launches": v[1].value, "relaunches": v[2].value, "disabled": bool(dis.value)}
 
 
 def set_option(option, value):

@@ -215,6 +215,8 @@ int main(int argc, char** argv) {
         std::ofstream(manifest) << lb.manifest_json() << "\n";
     }
     const Stats& s = lb.stats;
+    long long worker_calls = 0;  // small calls the resident call worker took (ECG_CALL_WORKER)
+    (void)ecg_call_worker_stats(&worker_calls, nullptr, nullptr, nullptr);
     printf("{\"ec_type\": %d, \"k\": %d, \"m\": %d, \"block_size\": %zu, \"stripes\": %d, \"store\": \"%s\", "
            "\"partial_decoding\": %s, \"sets\": %ld, \"repairs\": %ld, \"repairs_ok_pre_merge\": [%ld, %ld], "
            "\"repairs_ok_post_merge\": [%ld, %ld], \"repairs_failed\": %ld, \"skipped_undecodable\": %ld, "
@@ -224,14 +226,15 @@ int main(int argc, char** argv) {
            "\"merged_parities\": %ld, \"final_stripes\": %zu, \"gets_ok\": %ld, \"get_mismatch\": %ld, "
            "\"degraded_gets\": %ld, \"degraded_ok\": %ld, "
            "\"ecg_errors\": %ld, \"decode_undecodable\": %ld, \"blocks_in_store\": %zu, \"seconds\": {\"set\": %.4f, \"repair\": %.4f, "
-           "\"merge\": %.4f, \"get\": %.4f}, \"mismatches\": %s}\n",
+           "\"merge\": %.4f, \"get\": %.4f}, \"call_worker_calls\": %lld, \"mismatches\": %s}\n",
            schema.ec_type, schema.cp.k, schema.cp.m, schema.block_size, stripes, store_kind.c_str(),
            schema.partial_decoding ? "true" : "false", s.sets, s.repairs, pre_single, pre_multi, post_single,
            post_multi, s.repairs_failed, s.repairs_skipped_undecodable, s.repair_plans, s.plans_partial, s.plans_direct,
            s.blocks_rebuilt, s.rebuilt_mismatch, s.helper_messages, s.helper_bytes, merged ? "true" : "false",
            s.merges, s.merged_parities, lb.list_stripes().size(), get_ok, s.get_mismatch, degraded_tried, degraded_ok,
            s.ecg_errors,
-           s.decode_undecodable, store->count(), s.set_s, s.repair_s, s.merge_s, s.get_s, lb.mismatches_json().c_str());
+           s.decode_undecodable, store->count(), s.set_s, s.repair_s, s.merge_s, s.get_s, worker_calls,
+           lb.mismatches_json().c_str());
     // exit status: 0 = every repair rebuilt the lost bytes; mismatches are listed for the checker
     const bool pass = s.rebuilt_mismatch == 0 && s.get_mismatch == 0 && s.ecg_errors == 0 &&
                       s.repairs_failed == s.decode_undecodable &&

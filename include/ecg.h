@@ -52,6 +52,10 @@ int ecg_program_sets_retiring(void);
  * ever in flight at once, not by the number of threads that called (the reference's proxy starts a
  * thread per request, proxy.cpp:416-419). */
 int ecg_host_contexts(void);
+/* Resident call worker of the current device (ECG_OPT_CALL_WORKER), diagnostics: calls it completed,
+ * kernel launches (generations started), generations relaunched under a waiting call, and whether it is
+ * disabled after a failure (1) or not (0).  Any pointer may be NULL. */
+int ecg_call_worker_stats(long long* calls, long long* launches, long long* relaunches, int* disabled);
 /* The HIP runtime's pinned-transfer threshold for pageable host memory, in bytes, as this process runs
  * it: GPU_PINNED_MIN_XFER_SIZE (MiB) from the environment, default 1 MiB.  A pageable hipMemcpy of more
  * than this many bytes is pinned by the runtime for the copy (PCIe DMA rate); one of at most this many is
@@ -64,7 +68,7 @@ long long ecg_host_pinned_xfer_threshold(void);
 
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
  * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP, ECG_ZEROCOPY_BYTES, ECG_PROGRAM_CACHE, ECG_MAP_GROUP,
- * ECG_LAT_DWORD_BYTES).  Results never depend on them. */
+ * ECG_LAT_DWORD_BYTES, ECG_CALL_WORKER).  Results never depend on them. */
 #define ECG_OPT_NT 0           /* non-temporal policy: bit 0 = loads, bit 1 = stores (default 3) */
 #define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 128; 0 = auto (128 = 2 KiB) */
 #define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous, 2 = stripe s on XCD group s%8,
@@ -83,7 +87,14 @@ long long ecg_host_pinned_xfer_threshold(void);
                                      scope) with blocks of at most this many bytes run the latency kernel:
                                      4 bytes per lane, every input load in flight at once; 0 = never;
                                      default 1 MiB (profiles/r02/lat_kernel/) */
-#define ECG_OPT_COUNT 7
+#define ECG_OPT_CALL_WORKER 7 /* 0 = off (default); N > 0 = small synchronous host-tier calls (one op, <= 16
+                                 inputs, <= 4 outputs, blocks of at most 16 KiB, 4-byte multiples) go to a
+                                 resident kernel that polls a descriptor ring instead of launching one
+                                 kernel per call, and that kernel exits after N us without a call.  RS(6,4)
+                                 1 KiB: ~5 us instead of ~11 us per call.  The worker runs on a
+                                 high-priority stream: leave it off in a process that runs its own work on
+                                 high-priority streams */
+#define ECG_OPT_COUNT 8
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

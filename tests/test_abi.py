@@ -213,6 +213,10 @@ def test_tuning_options_validation(ecg):
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, -1) != 0
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_LAT_DWORD_BYTES, 0) == 0  # 16 bytes per lane always
         assert ecg.get_option(ecg.ECG_OPT_LAT_DWORD_BYTES) == 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_CALL_WORKER, -1) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_CALL_WORKER, 2_000_000) != 0  # idle limit above 1 s
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_CALL_WORKER, 500) == 0
+        assert ecg.get_option(ecg.ECG_OPT_CALL_WORKER) == 500
     finally:
         for o, v in enumerate(saved):
             ecg.set_option(o, v)
@@ -222,6 +226,8 @@ def test_tuning_options_validation(ecg):
         assert saved[ecg.ECG_OPT_MAP_GROUP] == 1
     if "ECG_LAT_DWORD_BYTES" not in os.environ:
         assert saved[ecg.ECG_OPT_LAT_DWORD_BYTES] == 1 << 20
+    if "ECG_CALL_WORKER" not in os.environ:
+        assert saved[ecg.ECG_OPT_CALL_WORKER] == 0  # off by default
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])

@@ -21,17 +21,20 @@ LIB = os.path.join(ROOT, "erasure-codes-prototype_amd", "lib", "libecg.so")
 
 def test_every_flag_kernel_of_libecg_has_the_full_release_sequence():
     ks, flagged, bad = C.check(C.disassemble(LIB))
-    # gf_lat_dword_kernel: 8 row tiles x 2 flavours x 6 input buckets x 2 (eager or not) = 192, and
+    # gf_lat_dword_kernel: 8 row tiles x 2 flavours x 6 input buckets x 2 (eager or not) = 192,
     # gf_vec_kernel in INLINE_LAT mode (mode 3): 8 x 2 x 4 NT policies = 64
     lat = [n for n in ks if "gf_lat_dword_kernel" in n]
     assert len(lat) == 192 and all(n in flagged for n in lat)
     inline_lat = re.compile(r"gf_vec_kernel<\d+, 3, \d+, (true|false)>")
     vec_lat = [n for n in ks if inline_lat.search(n)]
     assert len(vec_lat) == 64 and all(n in flagged for n in vec_lat)
-    assert len(flagged) == 256
+    # and the resident call worker (ECG_OPT_CALL_WORKER), which posts the same flags per call
+    worker = [n for n in ks if "gf_call_worker_kernel" in n]
+    assert len(worker) == 1 and worker[0] in flagged
+    assert len(flagged) == 257
     assert not bad, {n: p for n, p in list(bad.items())[:3]}
-    # no other kernel writes the L2 back (the batched kernels never post flags)
-    assert all("gf_lat_dword_kernel" in n or inline_lat.search(n) for n in flagged)
+    # no other kernel writes the L2 back to the host (the batched kernels never post flags)
+    assert all("gf_lat_dword_kernel" in n or inline_lat.search(n) or n in worker for n in flagged)
 
 
 def _probe(tmp_path, drop):
@@ -67,3 +70,8 @@ def test_checker_on_synthetic_sequences():
     assert any("not system scope" in p for p in C.check_kernel(not_system))
     store_after_barrier = good[:3] + ["global_store_dword v[4:5], v2, off"] + good[3:]
     assert C.check_kernel(store_after_barrier)
+    # an agent-scope write-back (the call worker publishing a descriptor to its other workgroups) is not a
+    # host flag: not checked, and a kernel with only such write-backs posts no flags
+    agent = ["global_store_dword v[2:3], v1, off", "buffer_wbl2 sc1", "global_store_dword v4, v5, s[2:3] sc1"]
+    assert C.check_kernel(agent) == []
+    assert not C.check("00000000 <k>:\n" + "\n".join("\t" + x for x in agent))[1]

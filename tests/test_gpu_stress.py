@@ -78,14 +78,19 @@ def _worker(tid, ecg, torch, n_ops, errors):
         errors.append((tid, repr(e)))
 
 
-def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle):
+@pytest.mark.parametrize("call_worker", [0, 2000])
+def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle, call_worker):
+    """... also with the resident call worker on (ECG_OPT_CALL_WORKER): it takes one thread's small host
+    calls at a time while the programs it reads are being evicted by the others."""
     import torch
     if not torch.cuda.is_available():
         pytest.fail("needs an MI355X")
     saved = ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE)
+    saved_worker = ecg.get_option(ecg.ECG_OPT_CALL_WORKER)
     errors = []
     try:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 8)
+        ecg.set_option(ecg.ECG_OPT_CALL_WORKER, call_worker)
         n_ops = int(os.environ.get("ECG_SOAK_OPS", "400"))  # longer soaks: ECG_SOAK_OPS=2000
         th = [threading.Thread(target=_worker, args=(t, ecg, torch, n_ops, errors)) for t in range(8)]
         [x.start() for x in th]
@@ -93,7 +98,11 @@ def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle):
         assert not any(x.is_alive() for x in th), "a worker hung"
     finally:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
+        ecg.set_option(ecg.ECG_OPT_CALL_WORKER, saved_worker)
     assert not errors, errors[:5]
+    if call_worker:
+        st = ecg.call_worker_stats()
+        assert st["calls"] > 0 and not st["disabled"], st
 
 
 def test_thread_per_request_resources_bounded(ecg, oracle):

@@ -13,9 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "erasure-codes-prototype_amd", "bin", "ecg_loopback")
 
 
-def run(args, timeout=600):
+def run(args, timeout=600, env=None):
     assert os.path.exists(BIN), "ecg_loopback not built (make -C erasure-codes-prototype_amd)"
-    p = subprocess.run([BIN] + args, capture_output=True, text=True, timeout=timeout)
+    p = subprocess.run([BIN] + args, capture_output=True, text=True, timeout=timeout,
+                       env=None if env is None else {**os.environ, **env})
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, p.stdout + p.stderr
     return p.returncode, json.loads(lines[-1]), p
@@ -47,10 +48,13 @@ def _objects(seed, k, B, n):
 
 
 @pytest.mark.gpu
-def test_config1_rs64_kv_store():
+@pytest.mark.parametrize("call_worker", ["0", "2000"])
+def test_config1_rs64_kv_store(call_worker):
     """config 1 as configured in project/config.ini (partial decoding on, OPTIMAL placement, x = 2) on
-    RS(6,4) as BASELINE.json names it: 64 stripes x 1 KiB."""
-    rc, s, p = run(["--ec", "RS", "--k", "6", "--m", "4", "--block-size", "1024", "--stripes", "64", "--x", "2"])
+    RS(6,4) as BASELINE.json names it: 64 stripes x 1 KiB; with kernel launches per call and with the
+    resident call worker taking the proxies' small calls (ECG_CALL_WORKER, the INTEGRATION.md setting)."""
+    rc, s, p = run(["--ec", "RS", "--k", "6", "--m", "4", "--block-size", "1024", "--stripes", "64", "--x", "2"],
+                   env={"ECG_CALL_WORKER": call_worker})
     assert rc == 0, p.stdout + p.stderr
     assert s["sets"] == 64 and s["gets_ok"] == 64 and s["get_mismatch"] == 0
     assert s["repairs_ok_pre_merge"] == [64 * 10, 64 * 5]  # every block of every stripe + 5 multi repairs
@@ -61,6 +65,7 @@ def test_config1_rs64_kv_store():
     assert s["blocks_in_store"] == 32 * 16  # old parities deleted, new ones written
     # degraded reads (proxy.cpp:517-666): one data block's datanode unreachable, rebuilt by ec->decode
     assert s["degraded_gets"] == 8 and s["degraded_ok"] == 8
+    assert (s["call_worker_calls"] > 0) == (call_worker != "0"), s["call_worker_calls"]
 
 
 @pytest.mark.gpu

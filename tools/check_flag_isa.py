@@ -12,6 +12,7 @@ every kernel that posts flags (it contains `buffer_wbl2`), the instruction strea
     global_store ... sc0 sc1  the flag (system scope; the first vector store after the write-back)
 
 (csrc/gf_done_flag.hpp).  Without the second wait the host read 3 of 2617 rebuilt blocks stale in round 2.
+Only system-scope write-backs count (`buffer_wbl2 sc0 sc1`); agent-scope ones stay on the device.
 The code object is taken from the library's .hip_fatbin section with objcopy + clang-offload-bundler in a
 temporary directory and disassembled with llvm-objdump; nothing is written into the repository.
 
@@ -61,13 +62,17 @@ def kernels(text):
     return out
 
 
+SYS_WBL2 = re.compile(r"^buffer_wbl2\b.*\bsc0\b.*\bsc1\b")
+
+
 def check_kernel(ins):
-    """Problems with the flag epilogue of one kernel's instruction list (empty = ok)."""
+    """Problems with the flag epilogues of one kernel's instruction list (empty = ok).  An epilogue is a
+    system-scope write-back (`buffer_wbl2 sc0 sc1`, what a release to the host compiles to); an agent-scope
+    one (`buffer_wbl2 sc1`, e.g. the call worker publishing a descriptor to its other workgroups) stays
+    on the device and is not a host flag."""
     probs = []
-    wbl = [i for i, x in enumerate(ins) if x.startswith("buffer_wbl2")]
+    wbl = [i for i, x in enumerate(ins) if SYS_WBL2.match(x)]
     for w in wbl:
-        if "sc0" not in ins[w] or "sc1" not in ins[w]:
-            probs.append(f"@{w} buffer_wbl2 is not system scope (sc0 sc1)")
         # the flag store: the first vector store after the write-back, with a vmcnt(0) wait before it
         f = next((i for i in range(w + 1, len(ins)) if STORE.match(ins[i])), None)
         if f is None:
@@ -94,7 +99,7 @@ def check_kernel(ins):
 def check(text):
     """(flag-posting kernels, {kernel: problems}) for a disassembly."""
     ks = kernels(text)
-    flagged = {n: ins for n, ins in ks.items() if any(x.startswith("buffer_wbl2") for x in ins)}
+    flagged = {n: ins for n, ins in ks.items() if any(SYS_WBL2.match(x) for x in ins)}
     bad = {n: p for n, ins in flagged.items() if (p := check_kernel(ins))}
     return ks, flagged, bad
 
