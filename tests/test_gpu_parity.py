@@ -1786,3 +1786,59 @@ def _batch_scope_layouts(ecg, oracle, torch, layout):
     torch.cuda.synchronize()
     for s in range(S):
         assert same([x.cpu().numpy() for x in blk[s]], want[s]), (layout, "decode", s)
+
+
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_replay_reference_repair_sequence(ecg, oracle, torch_cuda, form):
+    """bench.py's C++ caller of config 3's per-stripe sequence (loopback/replay.cpp): helper partial, main
+    partial and perform_addition per stripe through the C ABI -- one launch each (form 0), in scopes
+    (1) and in scopes with scratch partials (2) -- rebuilds every lost block (local repairs of every
+    data / local-parity block, Azure-LRC(12,2,2)), and the partials are never written in form 2."""
+    import sys
+    sys.argv = sys.argv[:1]
+    import bench
+    torch = torch_cuda
+    k, l, g, B, S = 12, 2, 2, 4096 + 16, 70
+    n = k + g + l
+    cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
+    ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)
+    M = ec.make_encoding_matrix()
+    st = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, 0x9E7 + form)
+    ecg.encode_batch(k, g + l, M, st[:, :k], st[:, k:])
+    cls_local = [e for e in range(n) if e not in (12, 13)]
+    splits = [bench.azure_local_split(e) for e in cls_local]
+    fail = torch.tensor(cls_local, dtype=torch.int32)
+    surv = torch.tensor([x[0] for x in splits], dtype=torch.int32).contiguous()
+    helper = torch.tensor([x[1][0] for x in splits], dtype=torch.int32).contiguous()
+    main = torch.tensor([x[1][1] for x in splits], dtype=torch.int32).contiguous()
+    stripe_of = torch.arange(S, dtype=torch.int32)
+    pattern_of = (torch.arange(S, dtype=torch.int32) % len(cls_local)).contiguous()
+    partials = torch.full((S, 2, B), 0x5A, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((S, B), dtype=torch.uint8, device="cuda")
+    rp = bench.replay_lib()
+    rc = rp.ecg_replay_partial_repair(ec._h, form, 16, st.data_ptr(), st.stride(0), st.stride(1), B, S,
+                                      stripe_of.data_ptr(), pattern_of.data_ptr(), fail.data_ptr(), 6, surv.data_ptr(),
+                                      3, helper.data_ptr(), 3, main.data_ptr(), partials.data_ptr(), out.data_ptr(),
+                                      out.stride(0), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, ecg.lib().ecg_last_error()
+    torch.cuda.synchronize()
+    idx = torch.arange(S, device="cuda")
+    lost = torch.tensor(cls_local, device="cuda")[pattern_of.cuda().long()]
+    assert torch.equal(out, st[idx, lost])
+    if form == 2:
+        assert bool((partials == 0x5A).all()), "scratch partials were written"
+        assert ecg.batch_last_stats()["composed"] == S - 64  # the last scope: 6 stripes, 3 calls -> 1 each
+    else:
+        assert not bool((partials == 0x5A).all())
+    # one repair against the oracle's own partial decoding (erasure_code.cpp:113-150)
+    from oracle import ec_ref as E
+    o = E.ec_factory(E.ECTYPE.AZURE_LRC, E.CodingParameters(k=k, l=l, g=g, local_or_column=True))
+    o.init_coding_parameters(E.CodingParameters(k=k, l=l, g=g, local_or_column=True))
+    host = st[3].cpu().numpy()
+    e, (sv, (hs, ms)) = cls_local[3], splits[3]
+    p0, p1 = E.zeros(1, B), E.zeros(1, B)
+    o.encode_partial_blocks_for_decoding([host[b] for b in hs], p0, B, hs, sv, [e])
+    o.encode_partial_blocks_for_decoding([host[b] for b in ms], p1, B, ms, sv, [e])
+    assert np.array_equal(p0[0] ^ p1[0], out[3].cpu().numpy())
