@@ -1510,7 +1510,10 @@ CallWorker g_worker[kMaxDevices];
 struct WorkerReaper {
     ~WorkerReaper() {
         for (CallWorker& w : g_worker) {
-            if (!w.ready || !w.running) continue;
+            // a thread still inside a call (detached threads run on during exit) keeps its worker: that
+            // generation leaves by itself within its idle time
+            std::unique_lock<std::mutex> lk(w.mu, std::try_to_lock);
+            if (!lk.owns_lock() || !w.ready || !w.running) continue;
             *w.stopw() = 1;
             const auto t0 = std::chrono::steady_clock::now();
             while (!w.gone() && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20)) __builtin_ia32_pause();
