@@ -1387,7 +1387,15 @@ struct CallWorker {
         running = false;
         return true;
     }
+    // Start a generation at call `start` (only while none is running).  The call's flags are cleared first:
+    // a generation that left (or was stopped) may have posted some of them for this very call, and the new
+    // one redoes the call from the start.  Flags left over from it would let the host finish the call
+    // while a workgroup of the new generation still rewrites the call's outputs -- into staging memory
+    // the host hands to the next call (seen as a wrong decode in the 8-thread x 2000 soak, where call
+    // sizes change and generations are restarted often).
     int launch(int workgroups, unsigned start) {
+        unsigned* f = flags() + (start % kWorkerSlots) * kWorkerMaxWG;
+        for (int w = 0; w < kWorkerMaxWG; w++) __atomic_store_n(&f[w], 0u, __ATOMIC_RELAXED);
         WorkerArgs a;
         memset(&a, 0, sizeof a);
         if (++gen == 0) ++gen;
