@@ -1342,7 +1342,8 @@ namespace {
 // exits (measured: 28 ms for one of 8 normal streams, none with the worker on a high-priority stream;
 // profiles/r03/persist/queue_interference.log).  A process that issues its own work on high-priority
 // streams shares that queue -- hence the option is off by default.  The worker exits by itself after the
-// option's idle time without a call (and after 50 ms in all), and at process exit.
+// option's idle time without a call, takes no call after 50 ms (the waiting call then starts the next
+// generation, so the queue is released at least that often), and stops at process exit.
 struct CallWorker {
     static constexpr double kLifeMs = 50.0;
     std::mutex mu;

@@ -362,8 +362,8 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLa
 // KB-bucket straight-line fold) over the workgroup's dword columns, and every workgroup posts its flag
 // with the same release sequence (gf_done_flag.hpp); it takes each call's inputs behind a system-scope
 // acquire, as a fresh launch would.  Bounded: a workgroup exits on the stop word, on
-// the leader's exit word, after idle_ticks without a call (followers wait twice as long), after
-// life_ticks in total or after max_polls polls -- whichever comes first -- and writes `gen` into its
+// the leader's exit word, after idle_ticks without a call or life_ticks in total (followers: twice both,
+// as a backstop) or after max_polls polls -- whichever comes first -- and writes `gen` into its
 // exit_info slot as it goes, so the host knows when the whole generation is gone.
 
 __device__ __forceinline__ unsigned long long wk_ptr(const unsigned* d, int q) {
@@ -417,13 +417,18 @@ __device__ __forceinline__ void worker_call_m(const unsigned* d) {
 
 __global__ void __launch_bounds__(kLatThreads, 1) gf_call_worker_kernel(const WorkerArgs a) {
     __shared__ unsigned d[64];
-    __shared__ unsigned go;
+    __shared__ unsigned go;  // set by thread 0 only: every exit decision is one for the whole workgroup
     const int tid = threadIdx.x;
     const bool leader = blockIdx.x == 0;
     unsigned next = a.start_seq;
     const unsigned long long t0 = wall_clock64();
     unsigned long long last = t0;
+    // The leader decides when a generation ends: on the stop word, after idle_ticks without a call, and --
+    // busy or not -- by not taking a call once life_ticks are over (the host then starts a new generation
+    // at that call).  It tells the others through the exit word; their own limits are twice as long, a
+    // backstop only: a follower leaving first would strand the calls the leader takes.
     const unsigned long long my_idle = leader ? a.idle_ticks : 2 * a.idle_ticks;
+    const unsigned long long my_life = leader ? a.life_ticks : 2 * a.life_ticks;
     for (unsigned polls = 0; polls < a.max_polls; polls++) {
         const unsigned slot = next % (unsigned)kWorkerSlots;
         if (leader) {
@@ -434,7 +439,12 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_call_worker_kernel(const Wo
                 if (tid == 0) go = stop ? 2u : 0u;
             }
             __syncthreads();
-            if (tid == 0 && go == 0 && d[0] == next && d[16] == next && d[32] == next && d[48] == next) go = 1;
+            if (tid == 0 && go == 0) {
+                const unsigned long long t = wall_clock64();
+                if (t - t0 > my_life) go = 2;
+                else if (d[0] == next && d[16] == next && d[32] == next && d[48] == next) go = 1;
+                else if (t - last > my_idle) go = 2;
+            }
             __syncthreads();
             if (go == 1 && gridDim.x > 1 && tid < 64) {  // republish for the followers: payload, then seq
                 __hip_atomic_store(&a.mbox[slot].w[tid], d[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -444,7 +454,8 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_call_worker_kernel(const Wo
             if (tid == 0) {
                 const unsigned sq = __hip_atomic_load(&a.mbseq[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned ex = __hip_atomic_load(&a.mbseq[kWorkerSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                go = sq == next ? 1u : ex == a.gen ? 2u : 0u;
+                const unsigned long long t = wall_clock64();
+                go = sq == next ? 1u : (ex == a.gen || t - last > my_idle || t - t0 > my_life) ? 2u : 0u;
             }
             __syncthreads();
             if (go == 1 && tid < 64)
@@ -454,8 +465,6 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_call_worker_kernel(const Wo
         const unsigned g = go;
         if (g == 2) break;
         if (g == 0) {
-            const unsigned long long t = wall_clock64();
-            if (t - last > my_idle || t - t0 > a.life_ticks) break;
             __syncthreads();  // d / go are rewritten by the next poll
             continue;
         }

@@ -205,3 +205,31 @@ def test_worker_does_not_hold_other_streams(worker, oracle, torch_cuda):
         s.synchronize()
         worst = max(worst, time.perf_counter() - t0)
     assert worst < 0.010, f"a stream waited {worst * 1e3:.1f} ms behind the worker"
+
+
+def test_worker_generation_ends_under_load(worker, oracle):
+    """Busy or not, a generation takes no call after its 50 ms lifetime: under a continuous stream of calls
+    the leader leaves, the waiting call starts the next generation, and no call is lost or wrong."""
+    ecg = worker
+    k, m, B = 6, 4, 1024
+    M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
+    rng = np.random.default_rng(77)
+    ecg.jerasure_matrix_encode(k, m, M, list(rnd(rng, k, B)), [np.zeros(B, np.uint8) for _ in range(m)], B)
+    st0 = ecg.call_worker_stats()
+    t0 = time.perf_counter()
+    n = bad = 0
+    while time.perf_counter() - t0 < 0.18:
+        data = list(rnd(rng, k, B))
+        out = [np.zeros(B, np.uint8) for _ in range(m)]
+        ref = [np.zeros(B, np.uint8) for _ in range(m)]
+        ecg.jerasure_matrix_encode(k, m, M, data, out, B)
+        oracle.jerasure_matrix_encode(k, m, M, data, ref, B)
+        bad += not all(np.array_equal(a, b) for a, b in zip(out, ref))
+        n += 1
+    st1 = ecg.call_worker_stats()
+    assert bad == 0
+    assert st1["calls"] - st0["calls"] == n
+    # 180 ms of calls: at least 3 generations, started by the call that found the last one gone or by one
+    # left waiting when it went
+    assert st1["launches"] - st0["launches"] >= 3, (st0, st1)
+    assert not st1["disabled"]
