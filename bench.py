@@ -13,7 +13,9 @@ Default workload (BASELINE.json configs[1], what the driver runs):
     per_rank  every rank's encode / decode kernel time and HBM fraction (all-gathered);
     config5   BASELINE.json configs[4] at this N: RS(10,4), 4 MiB, 65536 stripes sharded over the ranks
               in HBM-resident waves of 1024 -- aggregate GiB/s, every rank's HBM fraction, and the
-              combined parity checksum against the N = 1 value (--no-config5 skips it).
+              combined parity checksum against the N = 1 value (--no-config5 skips it);
+    ring_repair  (N > 1) config 3's partial decoding across neighbouring GPUs, partials over RCCL point to
+              point (the lrc-repair-ring workload, 1024 repairs per rank; --no-ring skips it).
 
 Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line):
   lrc-repair  configs[2]: Azure-LRC(12,2,2), 1 MiB, single-block repair of block s mod 16 of every
@@ -82,6 +84,8 @@ def parse():
     ap.add_argument("--config5-stripes", type=int, default=CONFIG5_STRIPES,
                     help="config 5's global stripe count, sharded over the ranks (BASELINE: 65536)")
     ap.add_argument("--config5-block-size", type=int, default=CONFIG5_BLOCK)
+    ap.add_argument("--no-ring", action="store_true",
+                    help="default workload at N > 1: skip the cross-GPU partial-decoding object (ring_repair)")
     ap.add_argument("--timeout", type=float, default=LAUNCH_TIMEOUT_S,
                     help="--gpus N > 1 started outside torch.distributed: wall-clock limit (s) on the ranks; "
                          "past it every rank is killed and bench.py exits 124")
@@ -355,6 +359,8 @@ def rs_encode_decode(a, r):
     torch.cuda.empty_cache()
     if not a.no_config5:
         line["config5"] = config5(a, r, M, k, m)
+    if r.world > 1 and not a.no_ring:
+        line["ring_repair"] = ring_repair_line(a, r)
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line
@@ -694,6 +700,37 @@ def ring_repair_state(r, S, B, chunk):
             ev[1].record()
 
     return step, rebuilt, e_main, main_view
+
+
+def ring_repair_line(a, r, S=1024, steps=5):
+    """The default line's `ring_repair` object at N > 1: config 3's partial decoding with the helper and
+    main proxies on neighbouring GPUs (lrc_repair_ring below), so that the first multi-GPU run of the
+    driver also moves partials over RCCL point to point (xGMI) and checks every repaired block.  An
+    exception here is reported in the object instead of failing the headline."""
+    B = 1 << 20
+    try:
+        torch.cuda.empty_cache()
+        step, rebuilt, e_main, main_view = ring_repair_state(r, S, B, 128)
+        rebuilt.zero_()
+        step()
+        torch.cuda.synchronize()
+        lost = main_view[torch.arange(S, device="cuda"), e_main]
+        ok = bool(torch.equal(rebuilt[:, 0], lost))
+        del lost
+        elapsed, _ = timed_loop(r, steps, step)
+        oks = D.gather_floats([1.0 if ok else 0.0], r, device="cuda")
+        out = {"workload": "Azure-LRC(12,2,2) local repair, 1 MiB, helper partials sent to the next rank over RCCL "
+                           "point to point, added in the main rank's fused kernel",
+               "backend": D._BACKEND,  # "nccl" = RCCL over xGMI; "gloo" only in the shared-GPU rehearsal
+               "stripes_per_gpu": S, "chunk_stripes": 128, "steps": steps,
+               "repairs_per_s": round(r.world * S * steps / elapsed, 1),
+               "xgmi_GBps_per_rank": round(S * B * steps / elapsed / 1e9, 1),
+               "verified_all_ranks": all(x[0] == 1.0 for x in oks)}
+        del step, rebuilt, e_main, main_view
+        torch.cuda.empty_cache()
+        return out
+    except Exception as e:  # noqa: BLE001 -- reported, the headline stands
+        return {"error": f"{type(e).__name__}: {str(e)[:300]}"}
 
 
 def lrc_repair_ring(a, r):

@@ -233,3 +233,29 @@ def test_worker_generation_ends_under_load(worker, oracle):
     # left waiting when it went
     assert st1["launches"] - st0["launches"] >= 3, (st0, st1)
     assert not st1["disabled"]
+
+
+def test_process_exits_promptly_with_a_resident_worker():
+    """A process that exits right after its calls, with the worker resident (idle limit 1 s), exits
+    promptly and cleanly: the reaper raises the stop word at exit and the worker leaves at its next poll
+    (its 50 ms lifetime would end it soon after anyway); no kernel is left running behind the process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, time, numpy as np; sys.path.insert(0, 'erasure-codes-prototype_amd'); import ecg\n"
+        "k, m, B = 6, 4, 1024\n"
+        "M = ecg.reed_sol_vandermonde_coding_matrix(k, m)\n"
+        "d = [np.full(B, j, np.uint8) for j in range(k)]\n"
+        "out = [np.zeros(B, np.uint8) for _ in range(m)]\n"
+        "for _ in range(3): ecg.jerasure_matrix_encode(k, m, M, d, out, B)\n"
+        "st = ecg.call_worker_stats()\n"
+        "assert st['calls'] >= 2, st\n"
+        "print('T_EXIT', time.time(), flush=True)\n")
+    env = dict(os.environ, ECG_CALL_WORKER="1000000")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    t_end = time.time()
+    assert p.returncode == 0, p.stderr[-2000:]
+    t_exit = float([ln for ln in p.stdout.splitlines() if ln.startswith("T_EXIT")][0].split()[1])
+    assert t_end - t_exit < 5.0, f"process took {t_end - t_exit:.2f} s to exit after its last call"

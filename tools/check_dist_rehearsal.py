@@ -30,6 +30,8 @@ for nm, x in (("N=1", rs1), ("N=2", rs2)):  # the default line's config5 object 
           f"stripes per rank {c5['stripes_per_rank']}, hbm_frac per rank {c5['hbm_frac_per_rank']}")
     ok &= c5["checksum_equals_n1"] is True and len(c5["hbm_frac_per_rank"]) == x["n_gpus"]
 print("per_rank", rs2["per_rank"])
+print("ring_repair N=2", rs2.get("ring_repair"))
+ok &= rs2.get("ring_repair", {}).get("verified_all_ranks") is True
 ok &= len(rs2["per_rank"]["encode_frac"]) == 2 and len(rs2["per_rank"]["decode_frac"]) == 2
 spawn = f"{d}/rs_n2_selfspawn.log"
 if os.path.exists(spawn):  # bench.py --gpus 2 started its own ranks (torch.distributed.run child)
