@@ -5,7 +5,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 R=$GRAFT_REPO_ROOT
-O=gpurun_out/r03a
+O=${O:-gpurun_out/r03a}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed" $O/pytest_gpu.log | tail -10
