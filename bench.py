@@ -14,8 +14,9 @@ Default workload (BASELINE.json configs[1], what the driver runs):
     config5   BASELINE.json configs[4] at this N: RS(10,4), 4 MiB, 65536 stripes sharded over the ranks
               in HBM-resident waves of 1024 -- aggregate GiB/s, every rank's HBM fraction, and the
               combined parity checksum against the N = 1 value (--no-config5 skips it);
-    ring_repair  (N > 1) config 3's partial decoding across neighbouring GPUs, partials over RCCL point to
-              point (the lrc-repair-ring workload, 1024 repairs per rank; --no-ring skips it).
+    ring_repair  config 3's partial decoding across neighbouring GPUs, partials over RCCL point to point
+              (the lrc-repair-ring workload, 1024 repairs per rank; --no-ring skips it); at N = 1 the
+              rank is its own RCCL peer, so the same RCCL path runs on one GPU (an on-GPU copy).
 
 Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line):
   lrc-repair  configs[2]: Azure-LRC(12,2,2), 1 MiB, single-block repair of block s mod 16 of every
@@ -75,6 +76,9 @@ def parse():
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
     ap.add_argument("--chunk", type=int, default=None, help="lrc-repair-ring: stripes per transfer")
+    ap.add_argument("--self-p2p", action="store_true",
+                    help="lrc-repair-ring at N = 1: rank 0 sends the partials to itself over RCCL point to point "
+                         "(the N > 1 nccl code path on one GPU; the rate is an intra-GPU copy, not xGMI)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--launch-check", action="store_true",
@@ -85,7 +89,7 @@ def parse():
                     help="config 5's global stripe count, sharded over the ranks (BASELINE: 65536)")
     ap.add_argument("--config5-block-size", type=int, default=CONFIG5_BLOCK)
     ap.add_argument("--no-ring", action="store_true",
-                    help="default workload at N > 1: skip the cross-GPU partial-decoding object (ring_repair)")
+                    help="default workload: skip the cross-GPU partial-decoding object (ring_repair)")
     ap.add_argument("--timeout", type=float, default=LAUNCH_TIMEOUT_S,
                     help="--gpus N > 1 started outside torch.distributed: wall-clock limit (s) on the ranks; "
                          "past it every rank is killed and bench.py exits 124")
@@ -363,7 +367,7 @@ def rs_encode_decode(a, r):
     torch.cuda.empty_cache()
     if not a.no_config5:
         line["config5"] = config5(a, r, M, k, m)
-    if r.world > 1 and not a.no_ring:
+    if not a.no_ring:
         line["ring_repair"] = ring_repair_line(a, r)
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
@@ -656,9 +660,11 @@ def replay_lib():
     return _REPLAY
 
 
-def ring_repair_state(r, S, B, chunk):
+def ring_repair_state(r, S, B, chunk, self_p2p=False):
     """Set-up of lrc-repair-ring (below) on rank r: returns (step, rebuilt, e_main, main_view); step()
-    runs one pipelined repair of the rank's S stripes.  tests/test_gpu_ring.py drives the same state."""
+    runs one pipelined repair of the rank's S stripes.  tests/test_gpu_ring.py drives the same state.
+    self_p2p (one rank over RCCL to itself): the helper's blocks get their own store, so the partials
+    really move from the helper's slot to the main proxy's."""
     k, l, g = 12, 2, 2
     n = k + g + l
     cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
@@ -682,7 +688,7 @@ def ring_repair_state(r, S, B, chunk):
 
     nxt = (r.rank + 1) % r.world
     main_store, main_view = make_store(r.rank)
-    help_store, help_view = (main_store, main_view) if r.world == 1 else make_store(nxt)
+    help_store, help_view = (main_store, main_view) if (r.world == 1 and not self_p2p) else make_store(nxt)
     idx = torch.arange(S, device="cuda", dtype=torch.int32)
     prog_main = ((idx + r.rank * S) % len(cls_local)).contiguous()
     prog_help = ((idx + nxt * S) % len(cls_local)).contiguous()
@@ -707,14 +713,19 @@ def ring_repair_state(r, S, B, chunk):
 
 
 def ring_repair_line(a, r, S=1024, steps=5):
-    """The default line's `ring_repair` object at N > 1: config 3's partial decoding with the helper and
-    main proxies on neighbouring GPUs (lrc_repair_ring below), so that the first multi-GPU run of the
-    driver also moves partials over RCCL point to point (xGMI) and checks every repaired block.  An
+    """The default line's `ring_repair` object: config 3's partial decoding with the helper and main
+    proxies on neighbouring GPUs (lrc_repair_ring below), so that every multi-GPU run of the driver also
+    moves partials over RCCL point to point (xGMI) and checks every repaired block.  At N = 1 the one rank
+    is its own RCCL peer (ecg_dist.init_self_p2p): the same RCCL code path, the partials copied on the one
+    GPU, so each N = 1 run exercises it on hardware too (its GB/s is an on-GPU copy, not xGMI).  An
     exception here is reported in the object instead of failing the headline."""
     B = 1 << 20
+    self_p2p = r.world == 1
     try:
         torch.cuda.empty_cache()
-        step, rebuilt, e_main, main_view = ring_repair_state(r, S, B, 128)
+        if self_p2p:
+            D.init_self_p2p(torch.device("cuda", torch.cuda.current_device()))
+        step, rebuilt, e_main, main_view = ring_repair_state(r, S, B, 128, self_p2p=self_p2p)
         rebuilt.zero_()
         step()
         torch.cuda.synchronize()
@@ -726,15 +737,19 @@ def ring_repair_line(a, r, S=1024, steps=5):
         out = {"workload": "Azure-LRC(12,2,2) local repair, 1 MiB, helper partials sent to the next rank over RCCL "
                            "point to point, added in the main rank's fused kernel",
                "backend": D._BACKEND,  # "nccl" = RCCL over xGMI; "gloo" only in the shared-GPU rehearsal
+               "self_p2p": self_p2p,  # N = 1: rank 0 is its own RCCL peer (on-GPU copy, not xGMI)
                "stripes_per_gpu": S, "chunk_stripes": 128, "steps": steps,
                "repairs_per_s": round(r.world * S * steps / elapsed, 1),
-               "xgmi_GBps_per_rank": round(S * B * steps / elapsed / 1e9, 1),
+               ("rccl_self_GBps" if self_p2p else "xgmi_GBps_per_rank"): round(S * B * steps / elapsed / 1e9, 1),
                "verified_all_ranks": all(x[0] == 1.0 for x in oks)}
         del step, rebuilt, e_main, main_view
         torch.cuda.empty_cache()
         return out
     except Exception as e:  # noqa: BLE001 -- reported, the headline stands
         return {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+    finally:
+        if self_p2p:
+            D.destroy()
 
 
 def lrc_repair_ring(a, r):
@@ -751,8 +766,13 @@ def lrc_repair_ring(a, r):
     B = a.block_size or (1 << 20)
     S = a.stripes or 1024
     # one rank: nothing to overlap, one launch per kernel; N > 1: 128 MiB transfers
-    chunk = max(1, min(S, a.chunk or (S if r.world == 1 else 128)))
-    step, rebuilt, e_main, main_view = ring_repair_state(r, S, B, chunk)
+    moves = r.world > 1 or a.self_p2p  # the partials cross RCCL
+    chunk = max(1, min(S, a.chunk or (128 if moves else S)))
+    if a.self_p2p:
+        if r.world != 1:
+            raise SystemExit("bench.py: --self-p2p is a one-rank mode")
+        D.init_self_p2p(torch.device("cuda", torch.cuda.current_device()))
+    step, rebuilt, e_main, main_view = ring_repair_state(r, S, B, chunk, self_p2p=a.self_p2p)
     rebuilt.zero_()
     for _ in range(a.warmup):
         step()
@@ -767,8 +787,10 @@ def lrc_repair_ring(a, r):
             "n_gpus": r.world, "stripes_per_gpu": S, "chunk_stripes": chunk, "steps": a.steps,
             "repairs_per_s": round(r.world * S * a.steps / elapsed, 1),
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "ms_per_step_rank0_events": round(t * 1e3, 3),
+            "backend": D._BACKEND if moves else None, "self_p2p": bool(a.self_p2p),
             "xgmi_bytes_per_rank_step": S * B if r.world > 1 else 0,
             "xgmi_GBps_per_rank": round(S * B * a.steps / elapsed / 1e9, 1) if r.world > 1 else 0.0,
+            "rccl_GBps_per_rank": round(S * B * a.steps / elapsed / 1e9, 1) if moves else 0.0,
             "hbm_executed_bytes_per_rank_step": 9 * S * B, "verified": ok, "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)"}
 
@@ -983,8 +1005,8 @@ def main():
     line = fn(a, r)
     if r.rank == 0:
         print(json.dumps(line), flush=True)
-    if r.distributed:
-        torch.distributed.destroy_process_group()
+    if r.distributed or D._SELF_P2P:
+        D.destroy()
 
 
 if __name__ == "__main__":

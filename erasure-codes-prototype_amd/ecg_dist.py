@@ -43,6 +43,11 @@ def from_env() -> Rank:
 
 
 _BACKEND = None
+# One rank exchanging with itself over RCCL (init_self_p2p): the ring's send / receive then go through RCCL
+# point to point (a copy on the one GPU) instead of staying in place, so a one-GPU box runs the exact nccl
+# code path of ring_exchange -- P2P ops, RCCL's stream, the current stream waiting on it -- that the
+# N > 1 ring runs over xGMI.
+_SELF_P2P = False
 
 # Seconds a rank waits in rendezvous or in any collective before it fails (ECG_DIST_TIMEOUT_S).  A rank
 # that never joins, or an RCCL communicator that never forms, then ends the run with an error instead of
@@ -63,6 +68,28 @@ def init(r: Rank, backend: str = "nccl", device=None) -> None:
         if device is not None:
             kw["device_id"] = device
         dist.init_process_group(backend, **kw)
+
+
+def init_self_p2p(device) -> None:
+    """A world-size-1 RCCL process group on `device` (127.0.0.1 rendezvous on a free port) whose ring
+    exchange sends to and receives from rank 0 itself; undo with destroy()."""
+    global _BACKEND, _SELF_P2P
+    if dist.is_initialized():
+        raise RuntimeError("init_self_p2p: a process group already exists")
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=timeout_s()), device_id=device)
+    _BACKEND, _SELF_P2P = "nccl", True
+
+
+def destroy() -> None:
+    global _SELF_P2P
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _SELF_P2P = False
 
 
 def stripe_range(total: int, r: Rank) -> tuple[int, int]:
@@ -170,10 +197,11 @@ class _Staged:
 def ring_exchange(send: torch.Tensor, recv: torch.Tensor, r: Rank):
     """Post send -> rank + 1 and recv <- rank - 1 (mod world) of two contiguous tensors of one shape;
     returns a handle whose wait() makes the data usable (on nccl: the current stream waits for RCCL's).
-    With one rank the block stays where it is (recv = send)."""
+    With one rank the block stays where it is (recv = send), unless init_self_p2p made rank 0 its own
+    RCCL peer."""
     if send.shape != recv.shape or not send.is_contiguous() or not recv.is_contiguous():
         raise ValueError("ring_exchange: send and recv must be contiguous tensors of one shape")
-    if not r.distributed:
+    if not r.distributed and not _SELF_P2P:
         if recv.data_ptr() != send.data_ptr():
             recv.copy_(send)
         return _Done()

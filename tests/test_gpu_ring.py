@@ -3,7 +3,10 @@ helper-partial and fused main kernels running on cuda:0, checked byte for byte a
 
 The world-size-2 case runs two processes that share cuda:0 (the pool's boxes have one GPU) and move
 the partials with gloo through host memory; on an 8-GPU node the same code moves them with RCCL over
-xGMI.  Each rank's repaired blocks are compared with the oracle's encode of the owner's stripes.
+xGMI.  RCCL refuses two ranks on one GPU, so its branch of ring_exchange runs here as one rank that is
+its own RCCL peer (ecg_dist.init_self_p2p): the partials leave the helper's store and arrive in the main
+proxy's through RCCL point-to-point ops, ordered with the kernels by the same stream waits.  Each rank's
+repaired blocks are compared with the oracle's encode of the owner's stripes.
 """
 import os
 import socket
@@ -36,10 +39,10 @@ def _expected(owner):
     return np.stack(out)
 
 
-def _run(r):
+def _run(r, self_p2p=False):
     import torch
     import bench
-    step, rebuilt, _, _ = bench.ring_repair_state(r, S, B, CHUNK)
+    step, rebuilt, _, _ = bench.ring_repair_state(r, S, B, CHUNK, self_p2p=self_p2p)
     rebuilt.zero_()
     step()
     torch.cuda.synchronize()
@@ -85,3 +88,35 @@ def test_ring_repair_two_ranks_shared_gpu(ecg, oracle):
     [p.join(timeout=30) for p in procs]
     assert [x[1] for x in res] == [True, True], res
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _self_p2p_worker(q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    try:
+        import torch
+        import ecg
+        import ecg_dist as D
+        torch.cuda.set_device(0)
+        ecg.lib().ecg_set_device(0)
+        D.init_self_p2p(torch.device("cuda", 0))
+        backend = torch.distributed.get_backend()
+        got = _run(D.Rank(0, 1, 0), self_p2p=True)
+        ok = np.array_equal(got, _expected(0))
+        D.destroy()
+        q.put((ok, backend, ""))
+    except Exception as e:  # noqa: BLE001
+        q.put((False, None, repr(e)))
+
+
+def test_ring_repair_rccl_self_exchange(ecg, oracle):
+    """The nccl branch of ring_exchange on hardware: one rank, its own RCCL peer, partials through RCCL."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_self_p2p_worker, args=(q,))
+    p.start()
+    ok, backend, err = q.get(timeout=100)
+    p.join(timeout=30)
+    assert ok, err
+    assert backend == "nccl"
+    assert p.exitcode == 0
