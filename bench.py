@@ -14,6 +14,8 @@ Default workload (BASELINE.json configs[1], what the driver runs):
     config5   BASELINE.json configs[4] at this N: RS(10,4), 4 MiB, 65536 stripes sharded over the ranks
               in HBM-resident waves of 1024 -- aggregate GiB/s, every rank's HBM fraction, and the
               combined parity checksum against the N = 1 value (--no-config5 skips it);
+    host_path RS(10,4) 1 MiB stripes in pinned host memory, encode and 1-erasure decode including the
+              PCIe copies (128 stripes per rank, every rank on its own link; --no-host-path skips it);
     ring_repair  config 3's partial decoding across neighbouring GPUs, partials over RCCL point to point
               (the lrc-repair-ring workload, 1024 repairs per rank; --no-ring skips it); at N = 1 the
               rank is its own RCCL peer, so the same RCCL path runs on one GPU (an on-GPU copy).
@@ -88,6 +90,8 @@ def parse():
     ap.add_argument("--config5-stripes", type=int, default=CONFIG5_STRIPES,
                     help="config 5's global stripe count, sharded over the ranks (BASELINE: 65536)")
     ap.add_argument("--config5-block-size", type=int, default=CONFIG5_BLOCK)
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="default workload: skip the host-path sub-object (pinned host batch incl. PCIe copies)")
     ap.add_argument("--no-ring", action="store_true",
                     help="default workload: skip the cross-GPU partial-decoding object (ring_repair)")
     ap.add_argument("--timeout", type=float, default=LAUNCH_TIMEOUT_S,
@@ -367,6 +371,8 @@ def rs_encode_decode(a, r):
     torch.cuda.empty_cache()
     if not a.no_config5:
         line["config5"] = config5(a, r, M, k, m)
+    if not a.no_host_path:
+        line["host_path"] = host_path_line(a, r, M, k, m)
     if not a.no_ring:
         line["ring_repair"] = ring_repair_line(a, r)
     if r.world == 1 and not a.no_cpu_baseline:
@@ -955,6 +961,49 @@ def rs_host(a, r):
     return {"workload": f"RS(10,4) 1 MiB, {S} stripes in pinned host memory, incl. PCIe H2D/D2H",
             "n_gpus": r.world, "results": res, "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device, copied to pinned host buffers)"}
+
+
+def host_path_line(a, r, M, k, m, S=128, chunk=16, runs=3):
+    """The default line's `host_path` object: the path as the proxy runs it, starting and ending in host
+    memory (north star: the rate including pinned hipMemcpyAsync).  RS(10,4) 1 MiB stripes in pinned host
+    memory, encode and single-erasure decode through the H2D -> kernel -> D2H pipelines
+    (ecg_encode_batch_host / ecg_decode_batch_host, `chunk` stripes per stage).  Every rank drives its own
+    GPU's PCIe link, so at N > 1 the aggregate shows how the links add up.  The encoded parities are
+    compared with the device-resident encode of the same bytes.  Reported, never the headline; an
+    exception is reported in the object."""
+    n, B = k + m, 1 << 20
+    try:
+        dev = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(dev, 0xEC0DE, word_offset=D.data_word_offset(r.rank * S, n, B))
+        ecg.encode_batch(k, m, M, dev[:, :k], dev[:, k:])
+        host = torch.empty((S, n, B), dtype=torch.uint8).pin_memory()
+        host[:, :k].copy_(dev[:, :k])
+        host[:, k:].zero_()
+        out = torch.empty((S, 1, B), dtype=torch.uint8).pin_memory()
+        res = {}
+        for name, fn in (("encode", lambda: ecg.encode_batch_host(k, m, M, host[:, :k], host[:, k:], chunk)),
+                         ("decode", lambda: ecg.decode_batch_host(k, m, M, 1, [3], host, h_out=out,
+                                                                  chunk_stripes=chunk))):
+            fn()
+            ts = []
+            for _ in range(runs):
+                D.barrier(r)
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            t = D.max_over_ranks(min(ts), r, device="cuda")
+            res[f"{name}_GiBps"] = round(r.world * S * k * B / t / 2 ** 30, 2)
+        ok = bool(torch.equal(host[:, k:].to("cuda", non_blocking=False), dev[:, k:])) and \
+            bool(torch.equal(out[:, 0].to("cuda"), dev[:, 3]))
+        oks = D.gather_floats([1.0 if ok else 0.0], r, device="cuda")
+        del dev, host, out
+        torch.cuda.empty_cache()
+        return {"workload": f"RS(10,4) 1 MiB, {S} stripes per GPU in pinned host memory, encode and 1-erasure "
+                            f"decode incl. PCIe H2D/D2H ({chunk}-stripe pipeline chunks)",
+                **res, "unit": "GiB/s of data (k*B per stripe), all ranks", "verified_all_ranks":
+                all(x[0] == 1.0 for x in oks)}
+    except Exception as e:  # noqa: BLE001 -- reported, the headline stands
+        return {"error": f"{type(e).__name__}: {str(e)[:300]}"}
 
 
 def launch_check(a, r):

@@ -32,6 +32,12 @@ for nm, x in (("N=1", rs1), ("N=2", rs2)):  # the default line's config5 object 
 print("per_rank", rs2["per_rank"])
 print("ring_repair N=2", rs2.get("ring_repair"))
 ok &= rs2.get("ring_repair", {}).get("verified_all_ranks") is True
+for nm, x in (("N=1", rs1), ("N=2", rs2)):  # RCCL self-exchange at N = 1, gloo in the shared-GPU N = 2
+    if nm == "N=1":
+        print("ring_repair N=1", x.get("ring_repair"))
+        ok &= x.get("ring_repair", {}).get("verified_all_ranks") is True
+    print(f"host_path {nm}", x.get("host_path"))
+    ok &= x.get("host_path", {}).get("verified_all_ranks") is True
 ok &= len(rs2["per_rank"]["encode_frac"]) == 2 and len(rs2["per_rank"]["decode_frac"]) == 2
 spawn = f"{d}/rs_n2_selfspawn.log"
 if os.path.exists(spawn):  # bench.py --gpus 2 started its own ranks (torch.distributed.run child)
