@@ -73,7 +73,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs-encode-decode",
-                    choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "lrc-repair-ring", "pc-merge",
+                    choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "lrc-repair-ring", "lrc-global-ring",
+                             "pc-merge",
                              "rs4m-waves", "rs-host"])
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
@@ -718,6 +719,78 @@ def ring_repair_state(r, S, B, chunk, self_p2p=False):
     return step, rebuilt, e_main, main_view
 
 
+AZURE_GLOBAL_HELPERS = [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9, 10, 11]]  # the OPTIMAL partition's data parts
+
+
+def global_ring_state(r, S, B, chunk, self_p2p=False):
+    """Set-up of lrc-global-ring on rank r: Azure-LRC(12,2,2) global-parity repairs with partial decoding
+    across GPUs.  Stripe i of rank q (global stripe q * S + i) loses global parity e = 12 + (i + q * S) % 2.
+    Its k = 12 survivors are the data blocks, which the OPTIMAL partition puts in four parts of three
+    ({0,1,2} ... {9,10,11}); the lost block's own part {14,15,12,13}, the main proxy, holds none of them.
+    Each part holds more than f = 1 survivor, so each sends one partial (handle_repair.cpp:169-176): the
+    helper at shift d = 1..4 is rank q + d, which computes part d - 1's partial of rank q's stripes
+    (encode_partial_blocks_for_decoding over the part, survivors = the 12 data blocks) and sends it to rank
+    q; the main proxy adds the four partials (perform_addition, handle_repair.cpp:371-376) in one 4 -> 1
+    launch.  Helpers on the same rank as their main proxy (shift a multiple of N) copy in place.  Returns
+    (step, rebuilt, e_main, main_view)."""
+    k, l, g = 12, 2, 2
+    n = k + g + l
+    # a global repair: the coordinator clears local_or_column (global partial-decoding matrices)
+    cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=False)
+    ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)
+    M = ec.make_encoding_matrix()
+    surv = list(range(k))
+    # program e - 12 of part p: the part's 3 coefficients of the lost global parity, written to slot 0
+    part_progs = [ecg.Programs([(ec.partial_decoding_matrix(part, surv, [e]), part, [0]) for e in (12, 13)])
+                  for part in AZURE_GLOBAL_HELPERS]
+    add4 = ecg.Programs([([[1, 1, 1, 1]], [0, 1, 2, 3], [0])])
+    stores = {}
+
+    def store(owner):  # the owner's S stripes, block-major [n][S][B] as in ring_repair_state
+        if owner not in stores:
+            st = torch.empty((n, S, B), dtype=torch.uint8, device="cuda")
+            ecg.fill_random(st, 0xEC0DE, word_offset=D.data_word_offset(owner * S, n + 1, B))
+            view = st.permute(1, 0, 2)
+            ecg.encode_batch(k, g + l, M, view[:, :k], view[:, k:n])
+            stores[owner] = (st, view)
+        return stores[owner]
+
+    main_store, main_view = store(r.rank)
+    idx = torch.arange(S, device="cuda", dtype=torch.int32)
+    owners = [(r.rank - d) % r.world for d in range(1, 5)]  # shift d: this rank helps owner q - d
+    helper_views = [store(o)[1] for o in owners]
+    prog_help = [((idx + o * S) % 2).contiguous() for o in owners]
+    e_main = (12 + (idx.long() + r.rank * S) % 2)
+    send = torch.empty((4, S, B), dtype=torch.uint8, device="cuda")  # send[d - 1]: partials for owner q - d
+    recv = torch.empty((4, S, B), dtype=torch.uint8, device="cuda")  # recv[d - 1]: from helper q + d
+    send_v, recv_v = send.permute(1, 0, 2), recv.permute(1, 0, 2)  # [S][4][B]
+    rebuilt = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
+
+    def helper(c0, c1):
+        for d in range(4):
+            ecg.matrix_apply_batch_multi(part_progs[d], helper_views[d][c0:c1], send_v[c0:c1, d:d + 1],
+                                         prog_of_stripe=prog_help[d][c0:c1])
+
+    def xchg(c0, c1):
+        if self_p2p or r.world > 1:
+            return D.exchange([(send[d, c0:c1], recv[d, c0:c1], -(d + 1)) for d in range(4)], r)
+        recv[:, c0:c1].copy_(send[:, c0:c1])  # one rank, no RCCL: every helper is local
+        return D.exchange([], r)
+
+    def main_(c0, c1):
+        ecg.matrix_apply_batch_multi(add4, recv_v[c0:c1], rebuilt[c0:c1])
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        D.pipelined_ring_repair(S, chunk, helper, main_, send, recv, r, xchg=xchg)
+        if ev:
+            ev[1].record()
+
+    return step, rebuilt, e_main, main_view
+
+
 def ring_repair_line(a, r, S=1024, steps=5):
     """The default line's `ring_repair` object: config 3's partial decoding with the helper and main
     proxies on neighbouring GPUs (lrc_repair_ring below), so that every multi-GPU run of the driver also
@@ -756,6 +829,41 @@ def ring_repair_line(a, r, S=1024, steps=5):
     finally:
         if self_p2p:
             D.destroy()
+
+
+def lrc_global_ring(a, r):
+    """Config 3's global-parity repairs with the helper proxies on four other GPUs (global_ring_state):
+    each repair gathers four 1 MiB partials over RCCL point to point (one exchange of four shifted pairs
+    per chunk) and adds them in one launch.  At N = 1 the helpers are local (a copy), or with --self-p2p
+    rank 0 is its own RCCL peer for all four."""
+    B = a.block_size or (1 << 20)
+    S = a.stripes or 256
+    moves = r.world > 1 or a.self_p2p
+    chunk = max(1, min(S, a.chunk or (32 if moves else S)))
+    if a.self_p2p:
+        if r.world != 1:
+            raise SystemExit("bench.py: --self-p2p is a one-rank mode")
+        D.init_self_p2p(torch.device("cuda", torch.cuda.current_device()))
+    step, rebuilt, e_main, main_view = global_ring_state(r, S, B, chunk, self_p2p=a.self_p2p)
+    rebuilt.zero_()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    lost = main_view[torch.arange(S, device="cuda"), e_main]
+    ok = bool(torch.equal(rebuilt[:, 0], lost))
+    del lost
+    assert ok, "global ring repair mismatch"
+    elapsed, evs = timed_loop(r, a.steps, step)
+    remote = sum(1 for d in range(1, 5) if d % r.world != 0) if r.world > 1 else (4 if a.self_p2p else 0)
+    return {"workload": "Azure-LRC(12,2,2) global-parity repair, 4 helper partitions on the next 4 GPUs, 1 MiB",
+            "n_gpus": r.world, "stripes_per_gpu": S, "chunk_stripes": chunk, "steps": a.steps,
+            "repairs_per_s": round(r.world * S * a.steps / elapsed, 1),
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "backend": D._BACKEND if moves else None, "self_p2p": bool(a.self_p2p),
+            "partials_over_rccl_per_repair": remote,
+            "rccl_GBps_per_rank": round(remote * S * B * a.steps / elapsed / 1e9, 1),
+            "hbm_algorithmic_bytes_per_repair": 13 * B, "verified": ok, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
 def lrc_repair_ring(a, r):
@@ -1049,7 +1157,7 @@ def main():
         D.init(r, "nccl", device=torch.device("cuda", dev) if r.distributed else None)
     ecg.lib().ecg_set_device(torch.cuda.current_device())
     fn = {"rs-encode-decode": rs_encode_decode, "rs-decode-patterns": rs_decode_patterns, "lrc-repair": lrc_repair,
-          "lrc-repair-ring": lrc_repair_ring, "pc-merge": pc_merge,
+          "lrc-repair-ring": lrc_repair_ring, "lrc-global-ring": lrc_global_ring, "pc-merge": pc_merge,
           "rs4m-waves": rs4m_waves, "rs-host": rs_host}[a.workload]
     line = fn(a, r)
     if r.rank == 0:

@@ -177,21 +177,39 @@ def gather_checksums(c: int, r: Rank, device="cpu") -> list[int]:
     return [int(x.item()) & _MASK64 for x in out]
 
 
-class _Done:
-    def wait(self):
-        return None
+def exchange(pairs, r: Rank):
+    """Post, for every (send, recv, shift) in `pairs`: send -> rank + shift and recv <- rank - shift (mod
+    world), all in one batch of RCCL point-to-point ops; returns a handle whose wait() makes every recv
+    usable (on nccl: the current stream waits for RCCL's).  send and recv of a pair are contiguous tensors of
+    one shape.  A pair whose peer is this rank itself (one rank, or a shift that is a multiple of the world
+    size: helper and main proxy on the same GPU) is a local copy -- unless init_self_p2p made rank 0 its own
+    RCCL peer, when it goes through RCCL like any other pair."""
+    for send, recv, _ in pairs:
+        if send.shape != recv.shape or not send.is_contiguous() or not recv.is_contiguous():
+            raise ValueError("exchange: send and recv must be contiguous tensors of one shape")
+    ops, staged = [], []
+    for i, (send, recv, shift) in enumerate(pairs):
+        dst, src = (r.rank + shift) % r.world, (r.rank - shift) % r.world
+        if dst == r.rank and not _SELF_P2P:
+            if recv.data_ptr() != send.data_ptr():
+                recv.copy_(send)
+            continue
+        if _BACKEND == "gloo" and send.is_cuda:  # gloo moves host tensors: stage the pair through host memory
+            hs = send.cpu()
+            hr = torch.empty_like(hs)
+            staged.append((hr, recv))
+            send, recv = hs, hr
+        # one tag per pair: gloo matches a recv to the send of the same pair index on the peer
+        ops += [dist.P2POp(dist.isend, send, dst, tag=i), dist.P2POp(dist.irecv, recv, src, tag=i)]
+    works = dist.batch_isend_irecv(ops) if ops else []
 
-
-class _Staged:
-    """gloo + CUDA tensors: gloo moves host tensors, so the chunk is staged through host memory."""
-
-    def __init__(self, works, host_recv, recv):
-        self.works, self.host_recv, self.recv = works, host_recv, recv
-
-    def wait(self):
-        for w in self.works:
-            w.wait()
-        self.recv.copy_(self.host_recv)
+    class _Works:
+        def wait(self):
+            for w in works:
+                w.wait()
+            for hr, recv in staged:
+                recv.copy_(hr)
+    return _Works()
 
 
 def ring_exchange(send: torch.Tensor, recv: torch.Tensor, r: Rank):
@@ -199,28 +217,10 @@ def ring_exchange(send: torch.Tensor, recv: torch.Tensor, r: Rank):
     returns a handle whose wait() makes the data usable (on nccl: the current stream waits for RCCL's).
     With one rank the block stays where it is (recv = send), unless init_self_p2p made rank 0 its own
     RCCL peer."""
-    if send.shape != recv.shape or not send.is_contiguous() or not recv.is_contiguous():
-        raise ValueError("ring_exchange: send and recv must be contiguous tensors of one shape")
-    if not r.distributed and not _SELF_P2P:
-        if recv.data_ptr() != send.data_ptr():
-            recv.copy_(send)
-        return _Done()
-    nxt, prv = (r.rank + 1) % r.world, (r.rank - 1) % r.world
-    if _BACKEND == "gloo" and send.is_cuda:
-        hs = send.cpu()
-        hr = torch.empty_like(hs)
-        works = dist.batch_isend_irecv([dist.P2POp(dist.isend, hs, nxt), dist.P2POp(dist.irecv, hr, prv)])
-        return _Staged(works, hr, recv)
-    works = dist.batch_isend_irecv([dist.P2POp(dist.isend, send, nxt), dist.P2POp(dist.irecv, recv, prv)])
-
-    class _Works:
-        def wait(self):
-            for w in works:
-                w.wait()
-    return _Works()
+    return exchange([(send, recv, 1)], r)
 
 
-def pipelined_ring_repair(n_stripes: int, chunk: int, helper, main, send, recv, r: Rank) -> None:
+def pipelined_ring_repair(n_stripes: int, chunk: int, helper, main, send, recv, r: Rank, xchg=None) -> None:
     """Cross-GPU partial decoding over a ring of ranks, chunk by chunk.
 
     Rank r is the helper proxy for the next rank's stripes and the main proxy for its own; stripe i's
@@ -229,14 +229,15 @@ def pipelined_ring_repair(n_stripes: int, chunk: int, helper, main, send, recv, 
       ring_exchange   -- send[c0:c1] -> rank + 1, recv[c0:c1] <- rank - 1 (queued behind the kernel)
       main(c0, c1)    -- after the chunk arrived: the main rank's fused kernel (own partial + addition)
     The main kernel of chunk c is issued after the helper kernel and the transfer of chunk c + 1, so
-    transfers run back to back while the kernels fill the gaps."""
+    transfers run back to back while the kernels fill the gaps.  xchg(c0, c1), when given, replaces the
+    single ring exchange (e.g. several helpers per stripe: one exchange() of several shifted pairs)."""
     if chunk < 1:
         raise ValueError("chunk must be >= 1")
     spans = [(c, min(c + chunk, n_stripes)) for c in range(0, n_stripes, chunk)]
     pending = None
     for c0, c1 in spans:
         helper(c0, c1)
-        h = ring_exchange(send[c0:c1], recv[c0:c1], r)
+        h = xchg(c0, c1) if xchg is not None else ring_exchange(send[c0:c1], recv[c0:c1], r)
         if pending is not None:
             pending[0].wait()
             main(*pending[1])

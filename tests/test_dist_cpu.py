@@ -173,6 +173,37 @@ def test_ring_partial_repair(world, S, chunk):
     assert res[0][2] == want
 
 
+def _exchange_worker(rank, world, port, q):
+    """ecg_dist.exchange with several shifted pairs in one batch (gloo, host tensors): pair d sends this
+    rank's block d to rank - d and receives rank + d's block d; a shift that is a multiple of the world
+    size stays on the rank (a copy)."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import ecg_dist as D
+    r = D.from_env()
+    D.init(r, backend="gloo")
+    send = [torch.full((3, 8), 16 * rank + d, dtype=torch.uint8) for d in range(1, 5)]
+    recv = [torch.zeros((3, 8), dtype=torch.uint8) for _ in range(4)]
+    D.exchange([(send[d - 1], recv[d - 1], -d) for d in range(1, 5)], r).wait()
+    ok = all(bool((recv[d - 1] == 16 * ((rank + d) % world) + d).all()) for d in range(1, 5))
+    q.put((rank, ok))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_shifted_pairs(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in procs]
+    res = sorted(q.get(timeout=120) for _ in procs)
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok in res), res
+
+
 def test_ring_exchange_single_rank_and_shape_checks():
     sys.path[:0] = [os.path.join(ROOT, "erasure-codes-prototype_amd")]
     import ecg_dist as D

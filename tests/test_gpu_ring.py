@@ -49,7 +49,7 @@ def _run(r, self_p2p=False):
     return rebuilt[:, 0].cpu().numpy()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, glob=False):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
@@ -61,8 +61,8 @@ def _worker(rank, world, port, q):
         ecg.lib().ecg_set_device(0)
         r = D.from_env()
         D.init(r, "gloo")
-        got = _run(r)
-        ok = np.array_equal(got, _expected(rank))
+        got = _run_global(r) if glob else _run(r)
+        ok = np.array_equal(got, _expected_global(rank) if glob else _expected(rank))
         torch.distributed.destroy_process_group()
         q.put((rank, ok, ""))
     except Exception as e:  # noqa: BLE001
@@ -74,7 +74,10 @@ def test_ring_repair_one_rank(ecg, oracle):
     assert np.array_equal(_run(D.Rank(0, 1, 0)), _expected(0))
 
 
-def test_ring_repair_two_ranks_shared_gpu(ecg, oracle):
+@pytest.mark.parametrize("glob", [False, True], ids=["local", "global"])
+def test_ring_repair_two_ranks_shared_gpu(ecg, oracle, glob):
+    """Two ranks on cuda:0 (gloo moves the partials).  Global repairs: helpers at shifts 1 and 3 are the
+    other rank, at 2 and 4 this rank itself (a local copy)."""
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -82,7 +85,7 @@ def test_ring_repair_two_ranks_shared_gpu(ecg, oracle):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, glob)) for r in range(2)]
     [p.start() for p in procs]
     res = sorted(q.get(timeout=100) for _ in procs)
     [p.join(timeout=30) for p in procs]
@@ -119,4 +122,66 @@ def test_ring_repair_rccl_self_exchange(ecg, oracle):
     p.join(timeout=30)
     assert ok, err
     assert backend == "nccl"
+    assert p.exitcode == 0
+
+
+def _expected_global(owner, S_=S):
+    """Oracle: the lost global parity 12 + (owner * S + i) % 2 of each of the owner's stripes
+    (bench.global_ring_state, same block-major splitmix layout as _expected)."""
+    from oracle import ec_ref as E
+    from oracle import ref
+    cp = E.CodingParameters(k=12, l=2, g=2, local_or_column=True)
+    ec = E.ec_factory(E.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)
+    out = []
+    for i in range(S_):
+        data = [ref.splitmix_bytes(0xEC0DE, (owner * S_ * 17 + j * S_ + i) * B // 8, B) for j in range(12)]
+        coding = E.zeros(4, B)
+        ec.encode(data, coding, B)
+        out.append(coding[(owner * S_ + i) % 2])
+    return np.stack(out)
+
+
+def _run_global(r, self_p2p=False):
+    import torch
+    import bench
+    step, rebuilt, _, _ = bench.global_ring_state(r, S, B, CHUNK, self_p2p=self_p2p)
+    rebuilt.zero_()
+    step()
+    torch.cuda.synchronize()
+    return rebuilt[:, 0].cpu().numpy()
+
+
+def test_global_ring_repair_one_rank(ecg, oracle):
+    import ecg_dist as D
+    assert np.array_equal(_run_global(D.Rank(0, 1, 0)), _expected_global(0))
+
+
+def _global_self_p2p_worker(q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    try:
+        import torch
+        import ecg
+        import ecg_dist as D
+        torch.cuda.set_device(0)
+        ecg.lib().ecg_set_device(0)
+        D.init_self_p2p(torch.device("cuda", 0))
+        got = _run_global(D.Rank(0, 1, 0), self_p2p=True)
+        ok = np.array_equal(got, _expected_global(0))
+        D.destroy()
+        q.put((ok, ""))
+    except Exception as e:  # noqa: BLE001
+        q.put((False, repr(e)))
+
+
+def test_global_ring_repair_rccl_self_exchange(ecg, oracle):
+    """Four helper partials per repair, all four through RCCL (rank 0 its own peer), vs the oracle."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_global_self_p2p_worker, args=(q,))
+    p.start()
+    ok, err = q.get(timeout=100)
+    p.join(timeout=30)
+    assert ok, err
     assert p.exitcode == 0
