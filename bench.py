@@ -17,8 +17,10 @@ Default workload (BASELINE.json configs[1], what the driver runs):
     host_path RS(10,4) 1 MiB stripes in pinned host memory, encode and 1-erasure decode including the
               PCIe copies (128 stripes per rank, every rank on its own link; --no-host-path skips it);
     ring_repair  config 3's partial decoding across neighbouring GPUs, partials over RCCL point to point
-              (the lrc-repair-ring workload, 1024 repairs per rank; --no-ring skips it); at N = 1 the
-              rank is its own RCCL peer, so the same RCCL path runs on one GPU (an on-GPU copy).
+              (the lrc-repair-ring workload, 1024 repairs per rank; --no-ring skips it and the next); at
+              N = 1 the rank is its own RCCL peer, so the same RCCL path runs on one GPU (an on-GPU copy);
+    global_ring_repair  the same for global-parity repairs, four helper partitions on ranks q+1..q+4
+              (lrc-global-ring, 256 repairs per rank, four partials each).
 
 Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line):
   lrc-repair  configs[2]: Azure-LRC(12,2,2), 1 MiB, single-block repair of block s mod 16 of every
@@ -376,6 +378,7 @@ def rs_encode_decode(a, r):
         line["host_path"] = host_path_line(a, r, M, k, m)
     if not a.no_ring:
         line["ring_repair"] = ring_repair_line(a, r)
+        line["global_ring_repair"] = ring_repair_line(a, r, S=256, glob=True)
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line
@@ -791,20 +794,25 @@ def global_ring_state(r, S, B, chunk, self_p2p=False):
     return step, rebuilt, e_main, main_view
 
 
-def ring_repair_line(a, r, S=1024, steps=5):
+def ring_repair_line(a, r, S=1024, steps=5, glob=False):
     """The default line's `ring_repair` object: config 3's partial decoding with the helper and main
     proxies on neighbouring GPUs (lrc_repair_ring below), so that every multi-GPU run of the driver also
     moves partials over RCCL point to point (xGMI) and checks every repaired block.  At N = 1 the one rank
     is its own RCCL peer (ecg_dist.init_self_p2p): the same RCCL code path, the partials copied on the one
     GPU, so each N = 1 run exercises it on hardware too (its GB/s is an on-GPU copy, not xGMI).  An
-    exception here is reported in the object instead of failing the headline."""
+    exception here is reported in the object instead of failing the headline.  glob: the `global_ring_repair`
+    object instead -- global-parity repairs whose four helper partitions sit on ranks q+1 .. q+4
+    (global_ring_state): four shifted exchanges per chunk, so at N >= 5 every rank sends on four xGMI links
+    and receives on four at once."""
     B = 1 << 20
     self_p2p = r.world == 1
+    chunk = 32 if glob else 128
     try:
         torch.cuda.empty_cache()
         if self_p2p:
             D.init_self_p2p(torch.device("cuda", torch.cuda.current_device()))
-        step, rebuilt, e_main, main_view = ring_repair_state(r, S, B, 128, self_p2p=self_p2p)
+        state = global_ring_state if glob else ring_repair_state
+        step, rebuilt, e_main, main_view = state(r, S, B, chunk, self_p2p=self_p2p)
         rebuilt.zero_()
         step()
         torch.cuda.synchronize()
@@ -813,13 +821,19 @@ def ring_repair_line(a, r, S=1024, steps=5):
         del lost
         elapsed, _ = timed_loop(r, steps, step)
         oks = D.gather_floats([1.0 if ok else 0.0], r, device="cuda")
-        out = {"workload": "Azure-LRC(12,2,2) local repair, 1 MiB, helper partials sent to the next rank over RCCL "
-                           "point to point, added in the main rank's fused kernel",
+        # partials that cross RCCL per repair (global: shifts that land on this rank itself are local copies)
+        moved = (sum(1 for d in range(1, 5) if d % r.world) if r.world > 1 else 4) if glob else 1
+        out = {"workload": ("Azure-LRC(12,2,2) global-parity repair, 1 MiB, the four helper partitions' partials "
+                            "sent from ranks q+1..q+4 over RCCL point to point, added in one launch") if glob else
+                           ("Azure-LRC(12,2,2) local repair, 1 MiB, helper partials sent to the next rank over RCCL "
+                            "point to point, added in the main rank's fused kernel"),
                "backend": D._BACKEND,  # "nccl" = RCCL over xGMI; "gloo" only in the shared-GPU rehearsal
                "self_p2p": self_p2p,  # N = 1: rank 0 is its own RCCL peer (on-GPU copy, not xGMI)
-               "stripes_per_gpu": S, "chunk_stripes": 128, "steps": steps,
+               "stripes_per_gpu": S, "chunk_stripes": chunk, "steps": steps,
                "repairs_per_s": round(r.world * S * steps / elapsed, 1),
-               ("rccl_self_GBps" if self_p2p else "xgmi_GBps_per_rank"): round(S * B * steps / elapsed / 1e9, 1),
+               "partials_over_rccl_per_repair": moved,
+               ("rccl_self_GBps" if self_p2p else "xgmi_GBps_per_rank"):
+                   round(moved * S * B * steps / elapsed / 1e9, 1),
                "verified_all_ranks": all(x[0] == 1.0 for x in oks)}
         del step, rebuilt, e_main, main_view
         torch.cuda.empty_cache()
