@@ -482,6 +482,11 @@ struct DeferScope {
     std::vector<DeferredCall> q;
     ScratchRanges scratch;
     FlushStats stats;
+    // the stream and device of the last group the scope launched: a scope flushes several times (every
+    // kEagerFlush calls, before a host-tier call, on ecg_batch_flush), and the first group of a flush must
+    // wait for the previous flush's last group when it runs on another stream
+    hipStream_t last_st = nullptr;
+    int last_dev = -1;
 };
 
 thread_local DeferScope t_defer;
@@ -574,6 +579,8 @@ int batch_begin() {
     t_defer.active = true;
     t_defer.q.clear();
     t_defer.scratch.clear();
+    t_defer.last_st = nullptr;
+    t_defer.last_dev = -1;
     return ECG_OK;
 }
 
@@ -1119,7 +1126,18 @@ int batch_flush() {
     (void)hipGetDevice(&caller_dev);
     cur_dev = caller_dev;
     int rc = ECG_OK;
-    hipStream_t prev_st = nullptr;
+    // the previous group: the last one of the scope's previous flush, if any
+    hipStream_t prev_st = d.last_st;
+    int prev_dev = d.last_dev;
+    auto set_dev = [&](int dev) {
+        if (dev == cur_dev) return ECG_OK;
+        if (hipSetDevice(dev) != hipSuccess) {
+            set_last_error("batch flush: hipSetDevice failed");
+            return ECG_EHIP;
+        }
+        cur_dev = dev;
+        return ECG_OK;
+    };
     for (size_t g = 0; g < groups.size() && rc == ECG_OK; g++) {
         const std::vector<size_t>& G = groups[g];
         const DeferredCall& c0 = q[G[0]];
@@ -1128,24 +1146,21 @@ int batch_flush() {
         // to the next, the new stream waits for an event recorded behind the previous group (so a chain
         // A, B, A orders every group after all earlier ones).  The calls were recorded in one order; a group
         // on stream B may read blocks an earlier group on A writes, or a scratch combination recorded on A
-        // (compose_scratch joins those to the op that forces them).  One stream: no event at all.
-        const bool switch_st = g > 0 && (c0.st != prev_st || eng->device() != cur_dev);
-        const int ev_dev = cur_dev;  // the previous group's device
-        if (switch_st && (rc = order_after(prev_st, ev_dev)) != ECG_OK) break;
-        if (eng->device() != cur_dev) {  // a group launches on the device its calls were recorded on
-            if (hipSetDevice(eng->device()) != hipSuccess) {
-                set_last_error("batch flush: hipSetDevice failed");
-                rc = ECG_EHIP;
-                break;
-            }
-            cur_dev = eng->device();
+        // (compose_scratch joins those to the op that forces them).  The chain runs across the scope's
+        // flushes too: the first group of a flush follows the last group of the previous one
+        // (test_batch_scope_orders_streams_across_eager_flushes).  One stream: no event at all.
+        const bool switch_st = prev_st != nullptr && (c0.st != prev_st || eng->device() != prev_dev);
+        if (switch_st) {  // the event is recorded behind the previous group, on that group's device
+            if ((rc = set_dev(prev_dev)) != ECG_OK || (rc = order_after(prev_st, prev_dev)) != ECG_OK) break;
         }
-        if (switch_st && hipStreamWaitEvent(c0.st, t_order_ev[ev_dev], 0) != hipSuccess) {
+        if ((rc = set_dev(eng->device())) != ECG_OK) break;  // a group launches on its calls' device
+        if (switch_st && hipStreamWaitEvent(c0.st, t_order_ev[prev_dev], 0) != hipSuccess) {
             set_last_error("batch flush: hipStreamWaitEvent failed");
             rc = ECG_EHIP;
             break;
         }
         prev_st = c0.st;
+        prev_dev = eng->device();
         if (G.size() == 1) {
             rc = eng->launch_direct(*c0.ops, c0.blocks.data(), c0.B, c0.st);
             st.launches += (long long)c0.ops->size();
@@ -1171,6 +1186,8 @@ int batch_flush() {
         }
     }
     if (cur_dev != caller_dev && caller_dev >= 0) (void)hipSetDevice(caller_dev);
+    d.last_st = prev_st;
+    d.last_dev = prev_dev;
     d.stats = st;
     return rc;
 }

@@ -1198,7 +1198,8 @@ def test_batch_scope_orders_streams(ecg, torch_cuda):
     want0 = ref[:, k] ^ ref[:, k + 1]
     want1 = ref[:, k + 2] ^ ref[:, k + 3] ^ ref[:, 0]
     torch.cuda.synchronize()
-    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    # B at high priority: a hardware queue of its own (two streams sharing one would run in order anyway)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
     ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
     for _ in range(2):
         out.zero_()
@@ -1217,6 +1218,43 @@ def test_batch_scope_orders_streams(ecg, torch_cuda):
         assert torch.equal(st, ref)
         assert torch.equal(out[:, 0], want0), "stream B read parities before stream A wrote them"
         assert torch.equal(out[:, 1], want1), "composed op on stream B did not see stream A's encode"
+
+
+def test_batch_scope_orders_streams_across_eager_flushes(ecg, torch_cuda):
+    """A scope without scratch flushes by itself every 1024 recorded calls, so a dependence can straddle two
+    flushes: 1024 encodes recorded on stream A fill the first flush, and the next flush starts with stream
+    B's additions of their parities.  B's first group must still wait for A (the scope keeps program order
+    across its flushes, not only inside one).  Stream A is kept busy beforehand, so B's kernels would run
+    long before A's encodes if they did not wait."""
+    torch = torch_cuda
+    k, m, S, B = 10, 4, 1024, 64 << 10
+    n = k + m
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    st = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(st, 0x0E7F)
+    ref = st.clone()
+    ecg.encode_batch(k, m, M, ref[:, :k], ref[:, k:])
+    want = ref[:, k] ^ ref[:, k + 1]
+    busy = torch.empty((512, n, 1 << 20), dtype=torch.uint8, device="cuda")  # 7 GiB of stripes
+    # B at high priority: HIP maps streams onto a few hardware queues, and two streams that share one run in
+    # queue order anyway, which would hide a missing wait; a high-priority stream has a queue of its own
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
+    out = torch.zeros((S, B), dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        out.zero_()
+        st[:, k:] = 0
+        torch.cuda.synchronize()
+        for _ in range(100):  # ~120 ms of encodes queued on A ahead of the scope's calls
+            ecg.encode_batch(k, m, M, busy[:, :k], busy[:, k:], stream=sa.cuda_stream)
+        with ecg.batch():
+            for s in range(S):  # exactly one eager flush's worth, all on A
+                ec.encode([st[s, j] for j in range(k)], [st[s, k + i] for i in range(m)], B, stream=sa.cuda_stream)
+            for s in range(S):  # the next flush opens with B
+                ec.perform_addition([st[s, k], st[s, k + 1]], [out[s]], B, 2, 1, stream=sb.cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(st, ref)
+        assert torch.equal(out, want), "stream B's first group of a flush ran before stream A's previous flush"
 
 
 def test_batch_scope_hazards_split_runs(ecg, torch_cuda):
@@ -1413,7 +1451,7 @@ def test_batch_scope_scratch_mid_scope_flush_and_streams(ecg, torch_cuda):
         assert ecg.batch_last_stats()["materialised"] == 2 * S
     # another stream reads a scratch partial: written for real first, on the producer's stream
     partials.fill_(0x3C)
-    side = torch.cuda.Stream()
+    side = torch.cuda.Stream(priority=-1)  # a hardware queue of its own: a missing wait would show
     with ecg.batch() as scope:
         scope.scratch(partials)
         for s, (e, surv, sets) in enumerate(plan):
