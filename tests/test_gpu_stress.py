@@ -87,10 +87,13 @@ def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle, call_worker):
         pytest.fail("needs an MI355X")
     saved = ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE)
     saved_worker = ecg.get_option(ecg.ECG_OPT_CALL_WORKER)
+    saved_zc = ecg.get_option(ecg.ECG_OPT_ZEROCOPY_BYTES)
     errors = []
     try:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 8)
         ecg.set_option(ecg.ECG_OPT_CALL_WORKER, call_worker)
+        if call_worker:  # the worker takes calls of the zero-copy host path only
+            ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, 8 << 20)
         n_ops = int(os.environ.get("ECG_SOAK_OPS", "400"))  # longer soaks: ECG_SOAK_OPS=2000
         th = [threading.Thread(target=_worker, args=(t, ecg, torch, n_ops, errors)) for t in range(8)]
         [x.start() for x in th]
@@ -99,6 +102,7 @@ def test_concurrent_mixed_tiers_with_cache_eviction(ecg, oracle, call_worker):
     finally:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
         ecg.set_option(ecg.ECG_OPT_CALL_WORKER, saved_worker)
+        ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, saved_zc)
     assert not errors, errors[:5]
     if call_worker:
         st = ecg.call_worker_stats()

@@ -25,14 +25,20 @@ def torch_cuda():
     return torch
 
 
+ZEROCOPY_DEFAULT = 8 << 20  # the worker takes calls of the zero-copy host path only
+
+
 @pytest.fixture()
 def worker(ecg, torch_cuda):
     saved = ecg.get_option(ecg.ECG_OPT_CALL_WORKER)
+    saved_zc = ecg.get_option(ecg.ECG_OPT_ZEROCOPY_BYTES)
     ecg.set_option(ecg.ECG_OPT_CALL_WORKER, 2000)  # exit after 2 ms without a call
+    ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, ZEROCOPY_DEFAULT)  # whatever ECG_ZEROCOPY_BYTES says
     try:
         yield ecg
     finally:
         ecg.set_option(ecg.ECG_OPT_CALL_WORKER, saved)
+        ecg.set_option(ecg.ECG_OPT_ZEROCOPY_BYTES, saved_zc)
 
 
 def rnd(rng, *shape):
@@ -253,7 +259,7 @@ def test_process_exits_promptly_with_a_resident_worker():
         "st = ecg.call_worker_stats()\n"
         "assert st['calls'] >= 2, st\n"
         "print('T_EXIT', time.time(), flush=True)\n")
-    env = dict(os.environ, ECG_CALL_WORKER="1000000")
+    env = dict(os.environ, ECG_CALL_WORKER="1000000", ECG_ZEROCOPY_BYTES=str(ZEROCOPY_DEFAULT))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env, cwd=root)
     t_end = time.time()
     assert p.returncode == 0, p.stderr[-2000:]

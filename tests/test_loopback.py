@@ -54,7 +54,8 @@ def test_config1_rs64_kv_store(call_worker):
     RS(6,4) as BASELINE.json names it: 64 stripes x 1 KiB; with kernel launches per call and with the
     resident call worker taking the proxies' small calls (ECG_CALL_WORKER, the INTEGRATION.md setting)."""
     rc, s, p = run(["--ec", "RS", "--k", "6", "--m", "4", "--block-size", "1024", "--stripes", "64", "--x", "2"],
-                   env={"ECG_CALL_WORKER": call_worker})
+                   env={"ECG_CALL_WORKER": call_worker,  # the worker rides on the zero-copy host path
+                        **({"ECG_ZEROCOPY_BYTES": str(8 << 20)} if call_worker != "0" else {})})
     assert rc == 0, p.stdout + p.stderr
     assert s["sets"] == 64 and s["gets_ok"] == 64 and s["get_mismatch"] == 0
     assert s["repairs_ok_pre_merge"] == [64 * 10, 64 * 5]  # every block of every stripe + 5 multi repairs
