@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs-encode-decode",
                     choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "lrc-repair-ring", "lrc-global-ring",
-                             "pc-merge",
+                             "pc-merge", "pc-merge-ring",
                              "rs4m-waves", "rs-host"])
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
@@ -794,6 +794,82 @@ def global_ring_state(r, S, B, chunk, self_p2p=False):
     return step, rebuilt, e_main, main_view
 
 
+def pc_bid(row, col):
+    """rowcol2bid (pc.cpp:326-340) of PC(4,1,4,1): data (row < 4, col < 4) = 4 row + col; the column
+    parities (row 4) = 20 + col."""
+    return row * 4 + col if row < 4 else 20 + col
+
+
+def pc_merge_ring_state(r, S, B, chunk, self_p2p=False):
+    """Set-up of pc-merge-ring on rank r: config 4's stripe merging with the two old stripes' clusters on
+    neighbouring GPUs.  PC(4,1,4,1), merge x = 2, HORIZONTAL: the merged PC(8,1,4,1)'s row parity `row` is
+    the XOR of the row's 4 blocks of old stripe 0 and 4 blocks of old stripe 1 (RS(8,1) rows are all ones;
+    main_recal / help_recal, handle_merge.cpp:159,269,319,453).  Merge i of rank q keeps old stripe 0 on
+    rank q (the main proxy, which writes the new parities) and old stripe 1 on rank q - 1 (the helper): the
+    helper XORs each row's 4 blocks into one partial (help_recal's encode_partial_blocks_for_encoding), the
+    5 partials of a merge travel to rank q (5 pairs of one exchange per chunk), and the main rank adds its
+    own 4 blocks per row and the received partial in one 5 -> 1 launch per row (perform_addition fused).
+    Stores are block-major [blocks][S][B], so each row's partials of a chunk are one contiguous region.
+    Returns (step, out, expected): out [S][5][B] gets the new row parities; expected(i0, i1) computes them
+    on the GPU from regenerated old stripes, for checking."""
+    nb = 25
+    gen = lambda owner, half, st: ecg.fill_random(  # noqa: E731 -- old stripe `half` of the owner's merges
+        st, 0xEC0DE, word_offset=D.data_word_offset((2 * owner + half) * S, nb, B))
+    main = torch.empty((nb + 5, S, B), dtype=torch.uint8, device="cuda")  # + 5 slots for received partials
+    gen(r.rank, 0, main[:nb])
+    nxt = (r.rank + 1) % r.world
+    helper = torch.empty((nb, S, B), dtype=torch.uint8, device="cuda")  # old stripe 1 of rank q + 1's merges
+    gen(nxt, 1, helper)
+    send = torch.empty((5, S, B), dtype=torch.uint8, device="cuda")
+    out = torch.empty((S, 5, B), dtype=torch.uint8, device="cuda")
+    main_v, help_v, send_v = main.permute(1, 0, 2), helper.permute(1, 0, 2), send.permute(1, 0, 2)
+    # one launch stripe per (merge, row): program `row` over merge i = stripe_of[i * 5 + row]
+    help_progs = ecg.Programs([([[1] * 4], [pc_bid(row, c) for c in range(4)], [row]) for row in range(5)])
+    main_progs = ecg.Programs([([[1] * 5], [pc_bid(row, c) for c in range(4)] + [nb + row], [row])
+                               for row in range(5)])
+    prog_of = (torch.arange(5 * S, device="cuda", dtype=torch.int32) % 5).contiguous()
+    stripe_of = (torch.arange(5 * S, device="cuda", dtype=torch.int32) // 5).contiguous()
+    moves = self_p2p or r.world > 1
+
+    def helper_k(c0, c1):
+        ecg.matrix_apply_batch_multi(help_progs, help_v, send_v, prog_of_stripe=prog_of[5 * c0:5 * c1],
+                                     stripe_of=stripe_of[5 * c0:5 * c1])
+
+    def xchg(c0, c1):
+        pairs = [(send[row, c0:c1], main[nb + row, c0:c1], 1) for row in range(5)]
+        if moves:
+            return D.exchange(pairs, r)
+        for snd, rcv, _ in pairs:  # one rank, no RCCL: the helper is local
+            rcv.copy_(snd)
+        return D.exchange([], r)
+
+    def main_k(c0, c1):
+        ecg.matrix_apply_batch_multi(main_progs, main_v, out, prog_of_stripe=prog_of[5 * c0:5 * c1],
+                                     stripe_of=stripe_of[5 * c0:5 * c1])
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        D.pipelined_ring_repair(S, chunk, helper_k, main_k, send, None, r, xchg=xchg)
+        if ev:
+            ev[1].record()
+
+    def expected(i0, i1):
+        """New row parities of this rank's merges [i0, i1): old stripe 1 regenerated here."""
+        own1 = torch.empty((nb, S, B), dtype=torch.uint8, device="cuda")
+        gen(r.rank, 1, own1)
+        want = torch.empty((i1 - i0, 5, B), dtype=torch.uint8, device="cuda")
+        for row in range(5):
+            x = torch.zeros((i1 - i0, B), dtype=torch.uint8, device="cuda")
+            for c in range(4):
+                x ^= main[pc_bid(row, c), i0:i1] ^ own1[pc_bid(row, c), i0:i1]
+            want[:, row] = x
+        del own1
+        return want
+
+    return step, out, expected
+
+
 def ring_repair_line(a, r, S=1024, steps=5, glob=False):
     """The default line's `ring_repair` object: config 3's partial decoding with the helper and main
     proxies on neighbouring GPUs (lrc_repair_ring below), so that every multi-GPU run of the driver also
@@ -877,6 +953,36 @@ def lrc_global_ring(a, r):
             "partials_over_rccl_per_repair": remote,
             "rccl_GBps_per_rank": round(remote * S * B * a.steps / elapsed / 1e9, 1),
             "hbm_algorithmic_bytes_per_repair": 13 * B, "verified": ok, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated on device)"}
+
+
+def pc_merge_ring(a, r):
+    """Config 4's stripe merging with the two old stripes' clusters on neighbouring GPUs (pc_merge_ring_state):
+    per merge, 5 row partials of 4 MiB travel over RCCL point to point and the main rank adds them in its
+    row launches.  At N = 1 the helper is local (a copy), or with --self-p2p rank 0 is its own RCCL peer."""
+    B = a.block_size or (4 << 20)
+    S = a.stripes or 64
+    moves = r.world > 1 or a.self_p2p
+    chunk = max(1, min(S, a.chunk or (8 if moves else S)))
+    if a.self_p2p:
+        if r.world != 1:
+            raise SystemExit("bench.py: --self-p2p is a one-rank mode")
+        D.init_self_p2p(torch.device("cuda", torch.cuda.current_device()))
+    step, out, expected = pc_merge_ring_state(r, S, B, chunk, self_p2p=a.self_p2p)
+    out.zero_()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    ok = all(bool(torch.equal(out[i:i + 16], expected(i, min(S, i + 16)))) for i in range(0, S, 16))
+    assert ok, "pc merge ring mismatch"
+    elapsed, _ = timed_loop(r, a.steps, step)
+    return {"workload": "PC(4,1,4,1) merge x=2 horizontal, 4 MiB, old stripes' clusters on neighbouring GPUs",
+            "n_gpus": r.world, "merges_per_gpu": S, "chunk_merges": chunk, "steps": a.steps,
+            "merges_per_s": round(r.world * S * a.steps / elapsed, 1),
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "backend": D._BACKEND if moves else None, "self_p2p": bool(a.self_p2p),
+            "rccl_GBps_per_rank": round(5 * S * B * a.steps / elapsed / 1e9, 1) if moves else 0.0,
+            "hbm_algorithmic_bytes_per_merge": 45 * B, "verified": ok, "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
@@ -1172,6 +1278,7 @@ def main():
     ecg.lib().ecg_set_device(torch.cuda.current_device())
     fn = {"rs-encode-decode": rs_encode_decode, "rs-decode-patterns": rs_decode_patterns, "lrc-repair": lrc_repair,
           "lrc-repair-ring": lrc_repair_ring, "lrc-global-ring": lrc_global_ring, "pc-merge": pc_merge,
+          "pc-merge-ring": pc_merge_ring,
           "rs4m-waves": rs4m_waves, "rs-host": rs_host}[a.workload]
     line = fn(a, r)
     if r.rank == 0:

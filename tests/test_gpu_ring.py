@@ -49,6 +49,18 @@ def _run(r, self_p2p=False):
     return rebuilt[:, 0].cpu().numpy()
 
 
+def _run_pc(r, self_p2p=False, S_=6, B_=8192):
+    """Config 4's merge with the clusters on neighbouring ranks; returns whether every new row parity equals
+    the XOR of the two old stripes' row blocks (recomputed with torch from regenerated stripes)."""
+    import torch
+    import bench
+    step, out, expected = bench.pc_merge_ring_state(r, S_, B_, 2, self_p2p=self_p2p)
+    out.zero_()
+    step()
+    torch.cuda.synchronize()
+    return bool(torch.equal(out, expected(0, S_)))
+
+
 def _worker(rank, world, port, q, glob=False):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -61,8 +73,11 @@ def _worker(rank, world, port, q, glob=False):
         ecg.lib().ecg_set_device(0)
         r = D.from_env()
         D.init(r, "gloo")
-        got = _run_global(r) if glob else _run(r)
-        ok = np.array_equal(got, _expected_global(rank) if glob else _expected(rank))
+        if glob == "pc":
+            ok = _run_pc(r)
+        else:
+            got = _run_global(r) if glob else _run(r)
+            ok = np.array_equal(got, _expected_global(rank) if glob else _expected(rank))
         torch.distributed.destroy_process_group()
         q.put((rank, ok, ""))
     except Exception as e:  # noqa: BLE001
@@ -74,7 +89,7 @@ def test_ring_repair_one_rank(ecg, oracle):
     assert np.array_equal(_run(D.Rank(0, 1, 0)), _expected(0))
 
 
-@pytest.mark.parametrize("glob", [False, True], ids=["local", "global"])
+@pytest.mark.parametrize("glob", [False, True, "pc"], ids=["local", "global", "pc-merge"])
 def test_ring_repair_two_ranks_shared_gpu(ecg, oracle, glob):
     """Two ranks on cuda:0 (gloo moves the partials).  Global repairs: helpers at shifts 1 and 3 are the
     other rank, at 2 and 4 this rank itself (a local copy)."""
@@ -180,6 +195,40 @@ def test_global_ring_repair_rccl_self_exchange(ecg, oracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_global_self_p2p_worker, args=(q,))
+    p.start()
+    ok, err = q.get(timeout=100)
+    p.join(timeout=30)
+    assert ok, err
+    assert p.exitcode == 0
+
+
+def test_pc_merge_ring_one_rank(ecg):
+    import ecg_dist as D
+    assert _run_pc(D.Rank(0, 1, 0))
+
+
+def _pc_self_p2p_worker(q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    try:
+        import torch
+        import ecg
+        import ecg_dist as D
+        torch.cuda.set_device(0)
+        ecg.lib().ecg_set_device(0)
+        D.init_self_p2p(torch.device("cuda", 0))
+        ok = _run_pc(D.Rank(0, 1, 0), self_p2p=True)
+        D.destroy()
+        q.put((ok, ""))
+    except Exception as e:  # noqa: BLE001
+        q.put((False, repr(e)))
+
+
+def test_pc_merge_ring_rccl_self_exchange(ecg):
+    """Config 4's merge partials (5 rows per merge) through RCCL, rank 0 its own peer."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_pc_self_p2p_worker, args=(q,))
     p.start()
     ok, err = q.get(timeout=100)
     p.join(timeout=30)

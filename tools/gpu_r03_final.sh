@@ -32,7 +32,7 @@ else
     timeout -k 10 500 python bench.py --workload $w --no-cpu-baseline > $O/bench_$w.log 2>&1
     rc=$?; echo "bench $w rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
-  for w in lrc-repair-ring lrc-global-ring; do
+  for w in lrc-repair-ring lrc-global-ring pc-merge-ring; do
     timeout -k 10 300 python bench.py --workload $w --self-p2p > $O/bench_$w.log 2>&1
     rc=$?; echo "bench $w --self-p2p rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
