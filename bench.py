@@ -20,7 +20,9 @@ Default workload (BASELINE.json configs[1], what the driver runs):
               (the lrc-repair-ring workload, 1024 repairs per rank; --no-ring skips it and the next); at
               N = 1 the rank is its own RCCL peer, so the same RCCL path runs on one GPU (an on-GPU copy);
     global_ring_repair  the same for global-parity repairs, four helper partitions on ranks q+1..q+4
-              (lrc-global-ring, 256 repairs per rank, four partials each).
+              (lrc-global-ring, 256 repairs per rank, four partials each);
+    merge_ring  configs[3]'s stripe merging with the old stripes' clusters on neighbouring GPUs
+              (pc-merge-ring, 64 merges per rank, five 4 MiB row partials each).
 
 Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line):
   lrc-repair  configs[2]: Azure-LRC(12,2,2), 1 MiB, single-block repair of block s mod 16 of every
@@ -379,6 +381,7 @@ def rs_encode_decode(a, r):
     if not a.no_ring:
         line["ring_repair"] = ring_repair_line(a, r)
         line["global_ring_repair"] = ring_repair_line(a, r, S=256, glob=True)
+        line["merge_ring"] = merge_ring_line(a, r)
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line
@@ -868,6 +871,40 @@ def pc_merge_ring_state(r, S, B, chunk, self_p2p=False):
         return want
 
     return step, out, expected
+
+
+def merge_ring_line(a, r, S=64, steps=5):
+    """The default line's `merge_ring` object: config 4's stripe merging with the old stripes' clusters on
+    neighbouring GPUs (pc_merge_ring_state), five 4 MiB row partials per merge over RCCL point to point; at
+    N = 1 the rank is its own RCCL peer.  Every new parity is checked; an exception is reported in the
+    object instead of failing the headline."""
+    B = 4 << 20
+    self_p2p = r.world == 1
+    try:
+        torch.cuda.empty_cache()
+        if self_p2p:
+            D.init_self_p2p(torch.device("cuda", torch.cuda.current_device()))
+        step, out, expected = pc_merge_ring_state(r, S, B, 8, self_p2p=self_p2p)
+        out.zero_()
+        step()
+        torch.cuda.synchronize()
+        ok = all(bool(torch.equal(out[i:i + 16], expected(i, min(S, i + 16)))) for i in range(0, S, 16))
+        elapsed, _ = timed_loop(r, steps, step)
+        oks = D.gather_floats([1.0 if ok else 0.0], r, device="cuda")
+        res = {"workload": "PC(4,1,4,1) merge x=2 horizontal, 4 MiB, old stripe 1's cluster on the previous rank: "
+                           "five row partials per merge over RCCL point to point, added in the main rank's row launches",
+               "backend": D._BACKEND, "self_p2p": self_p2p, "merges_per_gpu": S, "chunk_merges": 8, "steps": steps,
+               "merges_per_s": round(r.world * S * steps / elapsed, 1),
+               ("rccl_self_GBps" if self_p2p else "xgmi_GBps_per_rank"): round(5 * S * B * steps / elapsed / 1e9, 1),
+               "verified_all_ranks": all(x[0] == 1.0 for x in oks)}
+        del step, out, expected
+        torch.cuda.empty_cache()
+        return res
+    except Exception as e:  # noqa: BLE001 -- reported, the headline stands
+        return {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+    finally:
+        if self_p2p:
+            D.destroy()
 
 
 def ring_repair_line(a, r, S=1024, steps=5, glob=False):

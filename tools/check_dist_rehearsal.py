@@ -38,6 +38,8 @@ for nm, x in (("N=1", rs1), ("N=2", rs2)):  # RCCL self-exchange at N = 1, gloo 
         ok &= x.get("ring_repair", {}).get("verified_all_ranks") is True
     print(f"global_ring_repair {nm}", x.get("global_ring_repair"))
     ok &= x.get("global_ring_repair", {}).get("verified_all_ranks") is True
+    print(f"merge_ring {nm}", x.get("merge_ring"))
+    ok &= x.get("merge_ring", {}).get("verified_all_ranks") is True
     print(f"host_path {nm}", x.get("host_path"))
     ok &= x.get("host_path", {}).get("verified_all_ranks") is True
 ok &= len(rs2["per_rank"]["encode_frac"]) == 2 and len(rs2["per_rank"]["decode_frac"]) == 2
