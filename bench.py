@@ -97,6 +97,9 @@ def parse():
     ap.add_argument("--config5-block-size", type=int, default=CONFIG5_BLOCK)
     ap.add_argument("--no-host-path", action="store_true",
                     help="default workload: skip the host-path sub-object (pinned host batch incl. PCIe copies)")
+    ap.add_argument("--ring-scale", type=float, default=1.0,
+                    help="default workload: scale the cross-GPU objects' stripe / merge counts (rehearsals of many "
+                         "ranks on one GPU)")
     ap.add_argument("--no-ring", action="store_true",
                     help="default workload: skip the cross-GPU partial-decoding object (ring_repair)")
     ap.add_argument("--timeout", type=float, default=LAUNCH_TIMEOUT_S,
@@ -379,9 +382,10 @@ def rs_encode_decode(a, r):
     if not a.no_host_path:
         line["host_path"] = host_path_line(a, r, M, k, m)
     if not a.no_ring:
-        line["ring_repair"] = ring_repair_line(a, r)
-        line["global_ring_repair"] = ring_repair_line(a, r, S=256, glob=True)
-        line["merge_ring"] = merge_ring_line(a, r)
+        sc = lambda n: max(8, int(n * a.ring_scale)) // 8 * 8  # noqa: E731
+        line["ring_repair"] = ring_repair_line(a, r, S=sc(1024))
+        line["global_ring_repair"] = ring_repair_line(a, r, S=sc(256), glob=True)
+        line["merge_ring"] = merge_ring_line(a, r, S=sc(64))
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line

@@ -191,7 +191,7 @@ def _exchange_worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 5])
 def test_exchange_shifted_pairs(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
