@@ -551,6 +551,40 @@ bool strided_side(const std::vector<const uint8_t* const*>& calls, const std::ve
     return true;
 }
 
+// Fast path of a flush: every recorded call has the same plan (one interned object), stream, engine and
+// block size, and the blocks of all calls form one strided batch in which no two (call, block) pairs
+// overlap -- a per-stripe loop over one [S][n][B] batch, or over a block-major [n][S][B] one.  Then no call
+// reads or writes a block another call touches, so they form ONE group: what schedule_groups would
+// return, without hashing every block address.  Overlap-free when either
+//   (a) blocks of a call are >= B apart and whole stripes are apart: ss >= (vmax - vmin) * bs + B, or
+//   (b) calls are >= B apart and whole block rows are apart: bs >= (R - 1) * ss + B.
+bool one_disjoint_strided_group(const std::vector<DeferredCall>& q) {
+    const size_t R = q.size();
+    if (R < 2) return false;
+    const DeferredCall& a = q[0];
+    for (const DeferredCall& c : q)
+        if (c.ops.get() != a.ops.get() || c.st != a.st || c.B != a.B || c.eng != a.eng) return false;
+    thread_local std::vector<int> ids, v;
+    thread_local std::vector<const uint8_t* const*> calls;
+    ids.clear();
+    for (const LinearOp& op : *a.ops) {
+        ids.insert(ids.end(), op.src_ids.begin(), op.src_ids.end());
+        ids.insert(ids.end(), op.dst_ids.begin(), op.dst_ids.end());
+    }
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    calls.resize(R);
+    for (size_t c = 0; c < R; c++) calls[c] = q[c].blocks.data();
+    const uint8_t* base = nullptr;
+    long long ss = 0, bs = 0;
+    if (!strided_side(calls, ids, base, ss, bs, v)) return false;
+    const long long B = a.B;
+    const int vmin = *std::min_element(v.begin(), v.end()), vmax = *std::max_element(v.begin(), v.end());
+    if (vmax == vmin) return ss >= B;  // one block per call (or every id the same block)
+    if (bs < B) return false;
+    return ss >= (long long)(vmax - vmin) * bs + B || (ss >= B && bs >= (long long)(R - 1) * ss + B);
+}
+
 }  // namespace
 
 // A run of recorded calls whose blocks form one strided batch goes out as a strided launch (the
@@ -1108,19 +1142,24 @@ int batch_flush() {
     st.recorded = (long long)q.size();
     if (!d.scratch.empty()) q = compose_scratch(std::move(q), d.scratch, /*scope_end=*/!d.active, &st.materialised);
     st.composed = (long long)q.size();
-    PlanClasses classes;
-    std::vector<int> cls(q.size());
-    for (size_t c = 0; c < q.size(); c++) cls[c] = classes.of(q[c]);
-    auto reads = [&](size_t c, auto&& f) {
-        for (const LinearOp& op : *q[c].ops)
-            for (int id : op.src_ids) f(q[c].blocks[id]);
-    };
-    auto writes = [&](size_t c, auto&& f) {
-        for (const LinearOp& op : *q[c].ops)
-            for (int id : op.dst_ids) f(q[c].blocks[id]);
-    };
-    const std::vector<std::vector<size_t>> groups =
-        schedule_groups(q.size(), [&](size_t c) { return cls[c]; }, reads, writes);
+    std::vector<std::vector<size_t>> groups;
+    if (d.scratch.empty() && one_disjoint_strided_group(q)) {  // the per-stripe loop over one batch
+        groups.emplace_back(q.size());
+        std::iota(groups[0].begin(), groups[0].end(), (size_t)0);
+    } else {
+        PlanClasses classes;
+        std::vector<int> cls(q.size());
+        for (size_t c = 0; c < q.size(); c++) cls[c] = classes.of(q[c]);
+        auto reads = [&](size_t c, auto&& f) {
+            for (const LinearOp& op : *q[c].ops)
+                for (int id : op.src_ids) f(q[c].blocks[id]);
+        };
+        auto writes = [&](size_t c, auto&& f) {
+            for (const LinearOp& op : *q[c].ops)
+                for (int id : op.dst_ids) f(q[c].blocks[id]);
+        };
+        groups = schedule_groups(q.size(), [&](size_t c) { return cls[c]; }, reads, writes);
+    }
     st.groups = (long long)groups.size();
     int caller_dev = -1, cur_dev = -1;
     (void)hipGetDevice(&caller_dev);

@@ -1257,6 +1257,44 @@ def test_batch_scope_orders_streams_across_eager_flushes(ecg, torch_cuda):
         assert torch.equal(out, want), "stream B's first group of a flush ran before stream A's previous flush"
 
 
+def test_batch_scope_strided_fast_path_and_sliding_windows(ecg, torch_cuda):
+    """A flush whose calls share one plan and form one overlap-free strided batch takes one group without
+    the hazard hash (the per-stripe loop over [S][n][B] and over block-major [n][S][B]); a strided run whose
+    calls overlap -- a sliding window, call c encoding blocks c .. c+9 into c+10 .. c+13, every call
+    reading its predecessors' parities -- must not, and gives the sequential bytes."""
+    torch = torch_cuda
+    k, m, B = 10, 4, 4096
+    n = k + m
+    ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
+    for layout in ("stripe-major", "block-major"):
+        S = 300
+        buf = torch.empty((S, n, B) if layout == "stripe-major" else (n, S, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(buf, 0x5EED)
+        st = buf if layout == "stripe-major" else buf.permute(1, 0, 2)
+        ref = st.clone()
+        M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+        ecg.encode_batch(k, m, M, ref[:, :k], ref[:, k:])
+        with ecg.batch():
+            for s_ in range(S):
+                ec.encode([st[s_, j] for j in range(k)], [st[s_, k + i] for i in range(m)], B)
+        torch.cuda.synchronize()
+        assert torch.equal(st, ref), layout
+        assert ecg.batch_last_stats()["launches"] == 1, (layout, ecg.batch_last_stats())  # one group, one op
+    # sliding windows over one row of blocks: strided (stripe stride = one block) but overlapping
+    S = 200
+    row = torch.empty((S + n, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(row, 0x51DE)
+    want = row.clone()
+    for s_ in range(S):  # outside any scope: the sequential bytes
+        ec.encode([want[s_ + j] for j in range(k)], [want[s_ + k + i] for i in range(m)], B)
+    with ecg.batch():
+        for s_ in range(S):
+            ec.encode([row[s_ + j] for j in range(k)], [row[s_ + k + i] for i in range(m)], B)
+    torch.cuda.synchronize()
+    assert torch.equal(row, want), "sliding-window calls must keep their order"
+    assert ecg.batch_last_stats()["launches"] > 1
+
+
 def test_batch_scope_hazards_split_runs(ecg, torch_cuda):
     """Calls with the same plan that depend on each other (a chain of galois_region_xor-like additions
     through perform_addition) must keep their sequential meaning inside a scope."""
