@@ -106,7 +106,7 @@ def _ring_worker(rank, world, port, S, chunk, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import ecg_dist as D
-    from bench import azure_local_split
+    from ecg_ring import azure_local_split
     from oracle import ec_ref as E
     from oracle import ref
     r = D.from_env()

@@ -1390,7 +1390,7 @@ def test_batch_scope_flush_on_recording_device(ecg, torch_cuda):
 def _azure_repair_state(ecg, torch, S, B, seed):
     """Azure-LRC(12,2,2) stripes [S][16][B] on the GPU, block e = s mod 14 of stripe s lost (local repairs:
     data and local parities), with the helper / main split of handle_repair.cpp."""
-    from bench import azure_local_split
+    from ecg_ring import azure_local_split
     k, l, g = 12, 2, 2
     cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
     ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)

@@ -1,4 +1,5 @@
-"""Cross-GPU partial decoding on the GPU: bench.py's lrc-repair-ring state, with the
+"""Cross-GPU partial decoding on the GPU: ecg_ring's cross-GPU states (bench.py's
+lrc-repair-ring / lrc-global-ring / pc-merge-ring), with the
 helper-partial and fused main kernels running on cuda:0, checked byte for byte against the oracle.
 
 The world-size-2 case runs two processes that share cuda:0 (the pool's boxes have one GPU) and move
@@ -23,7 +24,7 @@ S, B, CHUNK = 20, 4096, 6
 
 def _expected(owner):
     """Oracle: the lost block of each of the owner's S stripes (block-major splitmix layout of
-    bench.ring_repair_state: block j of stripe i at word (owner * S * 17 + j * S + i) * B / 8)."""
+    ecg_ring.ring_repair_state: block j of stripe i at word (owner * S * 17 + j * S + i) * B / 8)."""
     from oracle import ec_ref as E
     from oracle import ref
     cp = E.CodingParameters(k=12, l=2, g=2, local_or_column=True)
@@ -41,8 +42,8 @@ def _expected(owner):
 
 def _run(r, self_p2p=False):
     import torch
-    import bench
-    step, rebuilt, _, _ = bench.ring_repair_state(r, S, B, CHUNK, self_p2p=self_p2p)
+    import ecg_ring
+    step, rebuilt, _, _ = ecg_ring.ring_repair_state(r, S, B, CHUNK, self_p2p=self_p2p)
     rebuilt.zero_()
     step()
     torch.cuda.synchronize()
@@ -53,8 +54,8 @@ def _run_pc(r, self_p2p=False, S_=6, B_=8192):
     """Config 4's merge with the clusters on neighbouring ranks; returns whether every new row parity equals
     the XOR of the two old stripes' row blocks (recomputed with torch from regenerated stripes)."""
     import torch
-    import bench
-    step, out, expected = bench.pc_merge_ring_state(r, S_, B_, 2, self_p2p=self_p2p)
+    import ecg_ring
+    step, out, expected = ecg_ring.pc_merge_ring_state(r, S_, B_, 2, self_p2p=self_p2p)
     out.zero_()
     step()
     torch.cuda.synchronize()
@@ -142,7 +143,7 @@ def test_ring_repair_rccl_self_exchange(ecg, oracle):
 
 def _expected_global(owner, S_=S):
     """Oracle: the lost global parity 12 + (owner * S + i) % 2 of each of the owner's stripes
-    (bench.global_ring_state, same block-major splitmix layout as _expected)."""
+    (ecg_ring.global_ring_state, same block-major splitmix layout as _expected)."""
     from oracle import ec_ref as E
     from oracle import ref
     cp = E.CodingParameters(k=12, l=2, g=2, local_or_column=True)
@@ -159,8 +160,8 @@ def _expected_global(owner, S_=S):
 
 def _run_global(r, self_p2p=False):
     import torch
-    import bench
-    step, rebuilt, _, _ = bench.global_ring_state(r, S, B, CHUNK, self_p2p=self_p2p)
+    import ecg_ring
+    step, rebuilt, _, _ = ecg_ring.global_ring_state(r, S, B, CHUNK, self_p2p=self_p2p)
     rebuilt.zero_()
     step()
     torch.cuda.synchronize()
