@@ -1188,7 +1188,9 @@ int batch_flush() {
         // (compose_scratch joins those to the op that forces them).  The chain runs across the scope's
         // flushes too: the first group of a flush follows the last group of the previous one
         // (test_batch_scope_orders_streams_across_eager_flushes).  One stream: no event at all.
-        const bool switch_st = prev_st != nullptr && (c0.st != prev_st || eng->device() != prev_dev);
+        // (prev_dev, not prev_st, says whether there was a previous group: the null stream -- torch's default
+        // stream -- is a stream like any other here)
+        const bool switch_st = prev_dev >= 0 && (c0.st != prev_st || eng->device() != prev_dev);
         if (switch_st) {  // the event is recorded behind the previous group, on that group's device
             if ((rc = set_dev(prev_dev)) != ECG_OK || (rc = order_after(prev_st, prev_dev)) != ECG_OK) break;
         }

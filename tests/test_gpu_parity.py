@@ -1178,12 +1178,14 @@ def test_batch_scope_eager_flush(ecg, torch_cuda, with_scratch):
     assert stats["recorded"] == (2 * S if with_scratch else (2 * S) % 1024), stats
 
 
-def test_batch_scope_orders_streams(ecg, torch_cuda):
+@pytest.mark.parametrize("a_null", [False, True], ids=["a_created", "a_null_stream"])
+def test_batch_scope_orders_streams(ecg, torch_cuda, a_null):
     """Calls recorded on two streams in one scope keep their recorded order: the flush makes a
     group wait for an event behind the previous group where the stream changes.  Stream A encodes a large
     batch; stream B then adds each stripe's first two parities (reads A's output); and a helper partial
     recorded on A into declared scratch is consumed by a perform_addition recorded on B (the composed op
-    runs on B and must see A's encode).  Without the ordering, B's kernels race A's."""
+    runs on B and must see A's encode).  Without the ordering, B's kernels race A's.  A is also torch's
+    default stream -- the null stream, handle 0, which the flush once took for "no previous group"."""
     torch = torch_cuda
     k, m, S, B = 10, 4, 256, 1 << 20
     n = k + m
@@ -1199,7 +1201,9 @@ def test_batch_scope_orders_streams(ecg, torch_cuda):
     want1 = ref[:, k + 2] ^ ref[:, k + 3] ^ ref[:, 0]
     torch.cuda.synchronize()
     # B at high priority: a hardware queue of its own (two streams sharing one would run in order anyway)
-    sa, sb = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
+    sa = torch.cuda.default_stream() if a_null else torch.cuda.Stream()
+    sb = torch.cuda.Stream(priority=-1)
+    assert (sa.cuda_stream == 0) == a_null
     ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=k, m=m))
     for _ in range(2):
         out.zero_()
@@ -1487,19 +1491,24 @@ def test_batch_scope_scratch_mid_scope_flush_and_streams(ecg, torch_cuda):
         torch.cuda.synchronize()
         assert torch.equal(partials, ref_p), "mid-scope flush must write pending scratch"
         assert ecg.batch_last_stats()["materialised"] == 2 * S
-    # another stream reads a scratch partial: written for real first, on the producer's stream
-    partials.fill_(0x3C)
+    # another stream reads a scratch partial: written for real first, on the producer's stream (torch's
+    # default stream, the null stream: the side read must wait for it -- it raced it in 1 run of 3 before
+    # the flush stopped taking handle 0 for "no previous group"; a few trials make such a race show)
     side = torch.cuda.Stream(priority=-1)  # a hardware queue of its own: a missing wait would show
-    with ecg.batch() as scope:
-        scope.scratch(partials)
-        for s, (e, surv, sets) in enumerate(plan):
-            for i in range(2):
-                ec.encode_partial_blocks_for_decoding([st[s, b] for b in sets[i]], [partials[s, i]], B, sets[i], surv, [e])
-        ec.perform_addition([partials[0, 0], partials[0, 1]], [out[0]], B, 2, 1, stream=side.cuda_stream)
-    torch.cuda.synchronize()
-    assert torch.equal(out[0], ref_o[0])
-    assert torch.equal(partials[0], ref_p[0])
-    assert bool((partials[1:] == 0x3C).all()), "unconsumed scratch must not be written at scope end"
+    for trial in range(12):
+        partials.fill_(0x3C)
+        out.zero_()
+        torch.cuda.synchronize()
+        with ecg.batch() as scope:
+            scope.scratch(partials)
+            for s, (e, surv, sets) in enumerate(plan):
+                for i in range(2):
+                    ec.encode_partial_blocks_for_decoding([st[s, b] for b in sets[i]], [partials[s, i]], B, sets[i], surv, [e])
+            ec.perform_addition([partials[0, 0], partials[0, 1]], [out[0]], B, 2, 1, stream=side.cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(out[0], ref_o[0]), f"trial {trial}: side-stream read raced the write-out"
+        assert torch.equal(partials[0], ref_p[0])
+        assert bool((partials[1:] == 0x3C).all()), "unconsumed scratch must not be written at scope end"
 
 
 def test_batch_scope_random_sequences(ecg, torch_cuda):
