@@ -248,7 +248,10 @@ void Engine::sweep_retired() {
             }
             r.armed = true;
         }
-        if (sync_all) (void)hipDeviceSynchronize();
+        if (sync_all) {
+            (void)hipGetLastError();  // the failed record is handled here: not a later call's error
+            (void)hipDeviceSynchronize();
+        }
         for (size_t i = 0; i < retired_.size();) {
             Retired& r = retired_[i];
             bool done = r.armed;

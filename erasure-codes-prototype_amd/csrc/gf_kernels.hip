@@ -705,6 +705,10 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         return hipErrorInvalidValue;
     if (base.B == 0) return hipSuccess;
     init_options();
+    // hipGetLastError after a launch names the thread's last error from ANY runtime call: clear what an
+    // earlier call left that its caller handled (e.g. the retirement's event on a stream the caller has
+    // destroyed since, which falls back to a device synchronize), so it is not taken for this launch's
+    (void)hipGetLastError();
     GfLaunch a = base;
     const long long vec_bytes = vec_ok ? (a.B & ~15LL) : 0;
     if (mode == GF_MODE_INLINE_LAT && vec_bytes == a.B && a.B <= g_opt[ECG_OPT_LAT_DWORD_BYTES].load() &&
@@ -781,6 +785,7 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
 
 hipError_t launch_call_worker(const WorkerArgs& a, int workgroups, hipStream_t st) {
     if (workgroups < 1 || workgroups > kWorkerMaxWG) return hipErrorInvalidValue;
+    (void)hipGetLastError();  // a handled earlier error is not this launch's (launch_gf)
     hipLaunchKernelGGL(gf_call_worker_kernel, dim3((unsigned)workgroups), dim3(kLatThreads), 0, st, a);
     return hipGetLastError();
 }
@@ -791,6 +796,7 @@ hipError_t launch_fill_splitmix(void* dst, long long nbytes, unsigned long long 
     const long long nwords = (nbytes + 7) >> 3;
     long long blocks = (nwords + kThreads - 1) / kThreads;
     if (blocks > 8192) blocks = 8192;
+    (void)hipGetLastError();  // a handled earlier error is not this launch's (launch_gf)
     hipLaunchKernelGGL(fill_splitmix_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st,
                        (uint8_t*)dst, nbytes, seed, word_offset);
     return hipGetLastError();
