@@ -333,7 +333,16 @@ def rs_encode_decode(a, r):
     # DESIGN.md §4); the outputs are checked after them -- every step rewrites the same bytes
     elapsed, evs = timed_loop(r, a.steps, step)
     idx = torch.arange(S, device="cuda")
-    assert torch.equal(rebuilt[:, 0], stripes[idx, idx % n]), "decode mismatch"  # outside the timing
+    # outside the timing: the timed decodes rebuilt the erased blocks, and one more decode with every erased
+    # block POISONED rebuilds the same bytes (so the kernel neither reads nor copies the block it rebuilds)
+    erased = stripes[idx, idx % n].clone()
+    assert torch.equal(rebuilt[:, 0], erased), "decode mismatch"
+    stripes[idx, idx % n] = 0xA5
+    rebuilt.zero_()
+    ecg.decode_batch(k, m, M, 1, patterns, stripes, out=rebuilt, pattern_of_stripe=pattern_of_stripe)
+    assert torch.equal(rebuilt[:, 0], erased), "decode mismatch with the erased blocks poisoned"
+    stripes[idx, idx % n] = erased
+    del erased
     checks = D.gather_checksums(D.checksum64(coding.contiguous()), r, device="cuda")
     enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
     dec_ms = [e[1].elapsed_time(e[2]) for e in evs]

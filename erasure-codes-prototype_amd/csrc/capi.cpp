@@ -58,6 +58,7 @@ void ecg_free(void* p) { free(p); }
 
 int ecg_program_cache_size(void) { return (int)Engine::instance().cache_size(); }
 int ecg_program_sets_retiring(void) { return (int)Engine::instance().retired_pending(); }
+int ecg_program_sets_reclaim(void) { return (int)Engine::instance().reclaim(); }
 int ecg_host_contexts(void) { return Engine::instance().host_contexts(); }
 
 int ecg_call_worker_stats(long long* calls, long long* launches, long long* relaunches, int* disabled) {

@@ -123,6 +123,32 @@ ProgramSet::~ProgramSet() {
     if (mem) owner->release_tables(mem, mem_class);
 }
 
+// A retirement cover: an event recorded on one stream after the set was retired; back to the pool when the
+// last set it covers is freed (it has fired by then, or the device was synchronized).
+struct ProgramSet::CoverEvent {
+    Engine* eng;
+    hipEvent_t ev;
+    ~CoverEvent() { eng->release_event(ev); }
+};
+
+hipEvent_t Engine::acquire_event() {
+    {
+        std::lock_guard<std::mutex> lk(pmu_);
+        if (!event_pool_.empty()) {
+            hipEvent_t ev = event_pool_.back();
+            event_pool_.pop_back();
+            return ev;
+        }
+    }
+    hipEvent_t ev = nullptr;
+    return hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess ? ev : nullptr;
+}
+
+void Engine::release_event(hipEvent_t ev) {
+    std::lock_guard<std::mutex> lk(pmu_);
+    event_pool_.push_back(ev);
+}
+
 // Before a launch on `st` reads the set's tables: once the upload event has fired the set is ready for
 // every stream; until then a launch on another stream than the uploading one waits for the event.
 int ProgramSet::ensure_ready(hipStream_t st) {
@@ -210,67 +236,168 @@ void Engine::release_tables(void* p, size_t cls) {
 
 void Engine::retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted) {
     std::lock_guard<std::mutex> lk(rmu_);
-    for (auto& ps : evicted) retired_.push_back(Retired{std::move(ps), {}, false});
+    for (auto& ps : evicted) retired_.push_back(std::move(ps));
 }
 
-void Engine::sweep_retired() {
-    std::vector<std::shared_ptr<ProgramSet>> dead;  // freed outside the lock
-    {
-        std::lock_guard<std::mutex> lk(rmu_);
-        if (retired_.empty()) return;
-        // events are created, recorded and (in the fallback) the device synchronized on THIS engine's
-        // device, whatever the calling thread's current device is
-        int caller_dev = -1;
-        (void)hipGetDevice(&caller_dev);
-        const bool switched = caller_dev != device_ && hipSetDevice(device_) == hipSuccess;
-        struct Restore {
-            bool on;
-            int dev;
-            ~Restore() {
-                if (on) (void)hipSetDevice(dev);
-            }
-        } restore{switched, caller_dev};
-        bool sync_all = false;
-        for (Retired& r : retired_) {
-            if (r.armed || r.ps.use_count() != 1) continue;
-            // nobody holds the set any more, so every launch that reads it is already enqueued
-            std::lock_guard<std::mutex> sk(r.ps->smu);
-            if (r.ps->overflow) sync_all = true;
-            for (int i = 0; i < r.ps->nstreams && !sync_all; i++) {
-                hipEvent_t ev = nullptr;
-                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
-                    hipEventRecord(ev, r.ps->streams[i]) != hipSuccess) {
-                    if (ev) (void)hipEventDestroy(ev);
-                    sync_all = true;  // e.g. a caller's stream destroyed since: fall back to the device
-                    break;
+namespace {
+bool never_destroyed(hipStream_t st) { return st == nullptr || st == hipStreamPerThread; }
+}  // namespace
+
+// One pass over the retired sets (ProgramSet's retirement comment):
+//   1. every unheld set's uncovered stream that may be named now -- `current` (a stream the caller handed
+//      the library in the call in progress) or a stream that is never destroyed -- gets a cover event,
+//      one record per stream per pass;
+//   2. sets whose covers (and upload) have all fired are freed;
+//   3. the cover mask is rebuilt from the streams still waiting;
+//   4. unheld sets that cannot be covered (streams not seen again, overflow) beyond kGraveyardMax: the
+//      device is synchronized and every unheld set freed.
+void Engine::sweep_retired(hipStream_t current, bool has_current) {
+    std::vector<std::shared_ptr<ProgramSet>> dead;  // destroyed after the lock is released
+    std::lock_guard<std::mutex> lk(rmu_);
+    sweep_locked(current, has_current, dead);
+}
+
+// A launch on st hit the cover mask: cover the unheld retired sets that wait for st (one event record).
+void Engine::cover_retired(hipStream_t st) {
+    std::lock_guard<std::mutex> lk(rmu_);
+    auto it = waiting_.find(st);
+    if (it == waiting_.end()) return;  // another stream with the same mask bit
+    std::shared_ptr<ProgramSet::CoverEvent> cover;
+    auto& v = it->second;
+    for (size_t i = 0; i < v.size();) {
+        std::shared_ptr<ProgramSet> ps = v[i].lock();
+        if (ps && ps.use_count() > 2) {  // still held by a caller (beyond retired_ and `ps`)
+            i++;
+            continue;
+        }
+        if (ps) {
+            if (!cover) {
+                hipEvent_t ev = acquire_event();
+                if (!ev) return;
+                if (hipEventRecord(ev, st) != hipSuccess) {
+                    release_event(ev);
+                    return;
                 }
-                r.evs.push_back(ev);
+                cover = std::make_shared<ProgramSet::CoverEvent>(ProgramSet::CoverEvent{this, ev});
             }
-            r.armed = true;
+            std::lock_guard<std::mutex> sk(ps->smu);
+            for (int e = 0; e < ps->nslots; e++)
+                if (ps->slots[e].st == st && !ps->slots[e].cover) ps->slots[e].cover = cover;
         }
-        if (sync_all) {
-            (void)hipGetLastError();  // the failed record is handled here: not a later call's error
-            (void)hipDeviceSynchronize();
-        }
-        for (size_t i = 0; i < retired_.size();) {
-            Retired& r = retired_[i];
-            bool done = r.armed;
-            for (size_t e = 0; done && e < r.evs.size(); e++) done = sync_all || hipEventQuery(r.evs[e]) == hipSuccess;
-            if (!done) {
-                i++;
-                continue;
-            }
-            for (hipEvent_t ev : r.evs) (void)hipEventDestroy(ev);
-            dead.push_back(std::move(r.ps));
-            retired_[i] = std::move(retired_.back());
-            retired_.pop_back();
-        }
+        v[i] = std::move(v.back());
+        v.pop_back();
+    }
+    if (v.empty()) {
+        waiting_.erase(it);
+        uint64_t mask = 0;
+        for (auto& kv : waiting_) mask |= stream_bit(kv.first);
+        cover_mask_.store(mask, std::memory_order_relaxed);
     }
 }
 
+void Engine::sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead) {
+    if (retired_.empty()) {
+        waiting_.clear();
+        cover_mask_.store(0, std::memory_order_relaxed);
+        return;
+    }
+    std::shared_ptr<ProgramSet::CoverEvent> made[3];  // current, null stream, per-thread stream
+    auto cover_for = [&](hipStream_t st) -> std::shared_ptr<ProgramSet::CoverEvent> {
+        const int i = (has_current && st == current) ? 0 : st == nullptr ? 1 : st == hipStreamPerThread ? 2 : -1;
+        if (i < 0) return nullptr;
+        if (!made[i]) {
+            hipEvent_t ev = acquire_event();
+            if (!ev) return nullptr;
+            if (hipEventRecord(ev, st) != hipSuccess) {
+                release_event(ev);
+                return nullptr;
+            }
+            made[i] = std::make_shared<ProgramSet::CoverEvent>(ProgramSet::CoverEvent{this, ev});
+        }
+        return made[i];
+    };
+    size_t graveyard = 0;
+    waiting_.clear();
+    for (size_t i = 0; i < retired_.size();) {
+        ProgramSet& ps = *retired_[i];
+        const bool unheld = retired_[i].use_count() == 1;
+        bool done = unheld;
+        {
+            std::lock_guard<std::mutex> sk(ps.smu);
+            for (int e = 0; e < ps.nslots; e++) {
+                ProgramSet::StreamSlot& sl = ps.slots[e];
+                if (!sl.cover && unheld && (never_destroyed(sl.st) || (has_current && sl.st == current)))
+                    sl.cover = cover_for(sl.st);
+                if (!sl.cover) {
+                    if (unheld) waiting_[sl.st].push_back(retired_[i]);
+                    done = false;
+                } else if (done) {
+                    done = hipEventQuery(sl.cover->ev) == hipSuccess;
+                }
+            }
+            if (ps.overflow) done = false;
+            if (done && !ps.ready.load(std::memory_order_acquire)) done = hipEventQuery(ps.ready_ev) == hipSuccess;
+        }
+        if (done) {
+            dead.push_back(std::move(retired_[i]));
+            retired_[i] = std::move(retired_.back());
+            retired_.pop_back();
+            continue;
+        }
+        if (unheld) graveyard++;
+        i++;
+    }
+    if (graveyard > kGraveyardMax) {
+        // on THIS engine's device, whatever the calling thread's current device is
+        int caller_dev = -1;
+        (void)hipGetDevice(&caller_dev);
+        const bool switched = caller_dev != device_ && hipSetDevice(device_) == hipSuccess;
+        const bool synced = hipDeviceSynchronize() == hipSuccess;
+        if (switched) (void)hipSetDevice(caller_dev);
+        if (synced) {
+            waiting_.clear();
+            for (size_t i = 0; i < retired_.size();) {
+                if (retired_[i].use_count() == 1) {
+                    dead.push_back(std::move(retired_[i]));
+                    retired_[i] = std::move(retired_.back());
+                    retired_.pop_back();
+                    continue;
+                }
+                i++;
+            }
+        }
+    }
+    uint64_t mask = 0;
+    for (auto& kv : waiting_) mask |= stream_bit(kv.first);
+    cover_mask_.store(mask, std::memory_order_relaxed);
+}
+
 size_t Engine::retired_pending() {
-    sweep_retired();
+    std::vector<std::shared_ptr<ProgramSet>> dead;
     std::lock_guard<std::mutex> lk(rmu_);
+    sweep_locked(nullptr, false, dead);
+    return retired_.size();
+}
+
+size_t Engine::reclaim() {
+    std::vector<std::shared_ptr<ProgramSet>> dead;
+    std::lock_guard<std::mutex> lk(rmu_);
+    int caller_dev = -1;
+    (void)hipGetDevice(&caller_dev);
+    const bool switched = caller_dev != device_ && hipSetDevice(device_) == hipSuccess;
+    const bool synced = hipDeviceSynchronize() == hipSuccess;
+    if (switched) (void)hipSetDevice(caller_dev);
+    if (!synced) return retired_.size();
+    for (size_t i = 0; i < retired_.size();) {
+        if (retired_[i].use_count() == 1) {
+            dead.push_back(std::move(retired_[i]));
+            retired_[i] = std::move(retired_.back());
+            retired_.pop_back();
+        } else {
+            i++;
+        }
+    }
+    sweep_locked(nullptr, false, dead);  // rebuilds the cover mask
     return retired_.size();
 }
 
@@ -390,7 +517,6 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
     if (!ps->pinned) return fail(e, "hipHostMalloc(program tables)");
     memcpy(ps->pinned, host.data(), total);
     ps->first_stream = st;
-    ps->used_on(st);
     if ((e = hipMemcpyAsync(ps->mem, ps->pinned, total, hipMemcpyHostToDevice, st)) != hipSuccess) {
         (void)hipStreamSynchronize(st);
         return fail(e, "hipMemcpyAsync(program tables)");
@@ -428,15 +554,15 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
         cache_.emplace(key, CacheEntry{ps, ++tick_});
     }
     if (!evicted.empty()) retire(std::move(evicted));
-    sweep_retired();
+    sweep_retired(st, true);  // st: the caller's stream, alive for this call
     return ps;
 }
 
 // One op over block pointers (device addresses), any k_in / m_out.  Ops that fit the kernel arguments
 // carry their pointers inline; wider ones (k_in > 128 or m_out > 32) go through an uploaded pointer
 // table (run_ptr_batch with one call), still asynchronous.
-int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st, bool latency,
-                       unsigned* flags, unsigned seq, int* n_flags) {
+int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t st, bool host_tier,
+                       bool latency, unsigned* flags, unsigned seq, int* n_flags) {
     if (n_flags) *n_flags = 0;
     if (op.m_out() == 0 || B == 0) return ECG_OK;
     if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
@@ -465,13 +591,13 @@ int Engine::launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, 
     for (int s : op.src_ids) vec_ok &= aligned16(blocks[s]);
     for (int j = 0; j < op.k_in(); j++) a.isrc[j] = blocks[op.src_ids[j]];
     for (int p = 0; p < op.m_out(); p++) a.idst[p] = blocks[op.dst_ids[p]];
-    ps->used_on(st);
     a.done_flags = latency ? flags : nullptr;
     a.done_seq = seq;
     // A single small call fills a few dozen workgroups: its time is the latency chain, not bandwidth, so
     // small blocks take the latency kernel (every load in flight at once) on the device tier as well.
     const bool lat = latency || (B <= get_option(ECG_OPT_LAT_DWORD_BYTES) && op.k_in() <= kLatMaxSrc);
     ECG_HIP(launch_gf(a, lat ? GF_MODE_INLINE_LAT : GF_MODE_INLINE, vec_ok, st, n_flags));
+    if (!host_tier) note_launch(*ps, st);
     return ECG_OK;
 }
 
@@ -487,9 +613,25 @@ struct DeferScope {
     FlushStats stats;
     // the stream and device of the last group the scope launched: a scope flushes several times (every
     // kEagerFlush calls, before a host-tier call, on ecg_batch_flush), and the first group of a flush must
-    // wait for the previous flush's last group when it runs on another stream
+    // wait for the previous flush's last group when it runs on another stream.  That stream is compared,
+    // never named: the caller may have destroyed it since (profiles/r04/stream/), so a flush that leaves the
+    // scope open records the ordering event behind its last group before it returns (last_recorded).
     hipStream_t last_st = nullptr;
     int last_dev = -1;
+    bool last_recorded = false;
+    // ordering events, one per device the scope launched on, leased from that device's engine pool for the
+    // scope and returned at its end (or at thread exit): none is held per thread between scopes
+    std::vector<std::pair<Engine*, hipEvent_t>> order_evs;
+    hipEvent_t order_ev(int dev) {
+        for (auto& e : order_evs)
+            if (e.first->device() == dev) return e.second;
+        return nullptr;
+    }
+    void release_order_evs() {
+        for (auto& e : order_evs) e.first->release_event(e.second);
+        order_evs.clear();
+    }
+    ~DeferScope() { release_order_evs(); }
 };
 
 thread_local DeferScope t_defer;
@@ -618,6 +760,7 @@ int batch_begin() {
     t_defer.scratch.clear();
     t_defer.last_st = nullptr;
     t_defer.last_dev = -1;
+    t_defer.last_recorded = false;
     return ECG_OK;
 }
 
@@ -768,7 +911,7 @@ public:
             // expressions reading blocks this call overwrites go out first, together as one op
             if (!uses_.empty()) {
                 fast_.clear();
-                start_collect(&fast_, c.eng, c.st, c.B);
+                start_collect(&fast_, c.eng, c.B);
                 for (const LinearOp& op : *c.ops)
                     for (int id : op.dst_ids) before_write(c.blocks[id]);
                 collect_ = nullptr;
@@ -874,7 +1017,7 @@ private:
             }
         }
         real_.clear();
-        start_collect(&real_, c.eng, c.st, c.B);
+        start_collect(&real_, c.eng, c.B);
         for (int p = 0; p < m; p++) {
             uint8_t* d = c.blocks[op.dst_ids[p]];
             if (scratch_->holds(d, c.B)) continue;
@@ -893,10 +1036,9 @@ private:
     // after the other stream's writes to the blocks the expression reads.  Written out on its own stream
     // instead, it would break the op's read-before-write when the two read each other's blocks (the
     // sequential interpreter of tests/sanitize/host_fuzz.cpp finds such cycles).
-    void start_collect(RowBuf* rows, Engine* eng, hipStream_t st, long long B) {
+    void start_collect(RowBuf* rows, Engine* eng, long long B) {
         collect_ = rows;
         ceng_ = eng;
-        cst_ = st;
         cB_ = B;
     }
 
@@ -941,7 +1083,7 @@ private:
                 eng = slab_[e].eng;
                 st = slab_[e].st;
                 B = slab_[e].B;
-                start_collect(&rows, eng, st, B);
+                start_collect(&rows, eng, B);
             }
             materialise(s);
         }
@@ -1041,7 +1183,6 @@ private:
     RowBuf* collect_ = nullptr;
     RowBuf real_, fast_, wo_;
     const Engine* ceng_ = nullptr;
-    hipStream_t cst_ = nullptr;
     long long cB_ = 0;
     std::vector<Terms> rows_;
     std::vector<uint8_t*> ins_;
@@ -1116,20 +1257,21 @@ private:
 
 }  // namespace
 
-// Per thread and device: the event batch_flush records behind a group when the next group runs on another
-// stream (created on first use and reused -- a wait takes the event's state at the time of the wait; only
-// threads whose scopes span streams create one, and it is not destroyed at thread exit, when the runtime
-// may already be going down).
-thread_local hipEvent_t t_order_ev[kMaxDevices] = {};
-
+// Record the scope's ordering event of device `dev` (the current device) behind the work enqueued on `st` so
+// far; `st` is a stream of the flush in progress, alive for the duration of the call.
 int order_after(hipStream_t st, int dev) {
     if (dev < 0 || dev >= kMaxDevices) return ECG_EINVAL;
-    if (!t_order_ev[dev] && hipEventCreateWithFlags(&t_order_ev[dev], hipEventDisableTiming) != hipSuccess) {
-        t_order_ev[dev] = nullptr;
-        set_last_error("batch flush: hipEventCreate failed");
-        return ECG_EHIP;
+    DeferScope& d = t_defer;
+    hipEvent_t ev = d.order_ev(dev);
+    if (!ev) {
+        Engine& eng = Engine::instance();  // the engine of the current device, dev
+        if (!(ev = eng.acquire_event())) {
+            set_last_error("batch flush: hipEventCreate failed");
+            return ECG_EHIP;
+        }
+        d.order_evs.emplace_back(&eng, ev);
     }
-    if (hipEventRecord(t_order_ev[dev], st) != hipSuccess) {
+    if (hipEventRecord(ev, st) != hipSuccess) {
         set_last_error("batch flush: hipEventRecord failed");
         return ECG_EHIP;
     }
@@ -1168,9 +1310,11 @@ int batch_flush() {
     (void)hipGetDevice(&caller_dev);
     cur_dev = caller_dev;
     int rc = ECG_OK;
-    // the previous group: the last one of the scope's previous flush, if any
+    // the previous group: the last one of the scope's previous flush, if any (its ordering event is then
+    // already recorded: that flush's stream is not named again)
     hipStream_t prev_st = d.last_st;
     int prev_dev = d.last_dev;
+    bool prev_recorded = d.last_recorded;
     auto set_dev = [&](int dev) {
         if (dev == cur_dev) return ECG_OK;
         if (hipSetDevice(dev) != hipSuccess) {
@@ -1194,17 +1338,18 @@ int batch_flush() {
         // (prev_dev, not prev_st, says whether there was a previous group: the null stream -- torch's default
         // stream -- is a stream like any other here)
         const bool switch_st = prev_dev >= 0 && (c0.st != prev_st || eng->device() != prev_dev);
-        if (switch_st) {  // the event is recorded behind the previous group, on that group's device
+        if (switch_st && !prev_recorded) {  // the event is recorded behind the previous group, on its device
             if ((rc = set_dev(prev_dev)) != ECG_OK || (rc = order_after(prev_st, prev_dev)) != ECG_OK) break;
         }
         if ((rc = set_dev(eng->device())) != ECG_OK) break;  // a group launches on its calls' device
-        if (switch_st && hipStreamWaitEvent(c0.st, t_order_ev[prev_dev], 0) != hipSuccess) {
+        if (switch_st && hipStreamWaitEvent(c0.st, d.order_ev(prev_dev), 0) != hipSuccess) {
             set_last_error("batch flush: hipStreamWaitEvent failed");
             rc = ECG_EHIP;
             break;
         }
         prev_st = c0.st;
         prev_dev = eng->device();
+        prev_recorded = false;
         if (G.size() == 1) {
             rc = eng->launch_direct(*c0.ops, c0.blocks.data(), c0.B, c0.st);
             st.launches += (long long)c0.ops->size();
@@ -1229,9 +1374,16 @@ int batch_flush() {
             if (rc != ECG_OK) break;
         }
     }
+    // the scope stays open: the next flush may start on another stream, so the last group's ordering event
+    // is recorded now, while its stream is certainly alive (one event record per flush)
+    if (rc == ECG_OK && d.active && prev_dev >= 0 && !prev_recorded) {
+        if ((rc = set_dev(prev_dev)) == ECG_OK) rc = order_after(prev_st, prev_dev);
+        prev_recorded = rc == ECG_OK;
+    }
     if (cur_dev != caller_dev && caller_dev >= 0) (void)hipSetDevice(caller_dev);
     d.last_st = prev_st;
     d.last_dev = prev_dev;
+    d.last_recorded = prev_recorded;
     d.stats = st;
     return rc;
 }
@@ -1244,6 +1396,7 @@ int batch_end() {
     const int rc = batch_flush();
     t_defer.q.clear();
     t_defer.scratch.clear();
+    t_defer.release_order_evs();  // a later wait on one refers to its record at the time of the wait
     return rc;
 }
 
@@ -1293,7 +1446,7 @@ int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* c
 
 int Engine::launch_direct(const std::vector<LinearOp>& ops, uint8_t* const* blocks, long long B, hipStream_t st) {
     for (const LinearOp& op : ops) {
-        int rc = launch_one(op, blocks, B, st);
+        int rc = launch_one(op, blocks, B, st, /*host_tier=*/false);
         if (rc != ECG_OK) return rc;
     }
     return ECG_OK;
@@ -1419,6 +1572,18 @@ struct CallWorker {
     unsigned long long ticks_per_us = 100;
     long long idle_us = 0, gen_idle_us = 0;  // the option now / the running generation's idle limit
     long long calls = 0, launches = 0, relaunches = 0;
+    // A call that does not complete within 100 ms (queued behind a long kernel, e.g.) turns the worker off
+    // for a cooldown that doubles per consecutive timeout (1 s .. 64 s); calls take the launch path meanwhile.
+    // `broken` stays for what cannot recover: initialisation failed.
+    std::chrono::steady_clock::time_point off_until{};
+    int timeouts_in_row = 0;
+    long long timeouts = 0;
+    bool cooling() const { return std::chrono::steady_clock::now() < off_until; }
+    void back_off() {
+        timeouts++;
+        const int sh = std::min(timeouts_in_row++, 6);
+        off_until = std::chrono::steady_clock::now() + std::chrono::seconds(1LL << sh);
+    }
 
     WorkerDesc* ring() { return (WorkerDesc*)host; }
     unsigned* flags() { return (unsigned*)(host + 1024); }
@@ -1508,7 +1673,7 @@ struct CallWorker {
     }
     // One call: 0 = done, 1 = not taken (use the launch path), < 0 = error.
     int call(int dev_id, const ProgramSet& ps, const LinearOp& op, uint8_t* const* dev, long long B) {
-        if (broken) return 1;
+        if (broken || cooling()) return 1;
         if (!ready && !init(dev_id)) {
             broken = true;
             return 1;
@@ -1539,7 +1704,7 @@ struct CallWorker {
         // a generation too narrow for this call, or started under another idle limit, makes way for a new one
         if (!gone() && (W < need || gen_idle_us != idle_us) && stop() != ECG_OK) return ECG_EHIP;
         if (!running && launch(std::max(need, 1), s) != ECG_OK) {
-            broken = true;
+            back_off();
             return 1;
         }
         const auto t0 = std::chrono::steady_clock::now();
@@ -1551,23 +1716,26 @@ struct CallWorker {
                 if (gone() && !done(slot, s)) {  // the generation left before taking the call: a new one takes it
                     relaunches++;
                     if (launch(std::max(need, W), s) != ECG_OK) {
-                        broken = true;
+                        back_off();
                         return 1;
                     }
                 }
             }
             if (t - t0 > std::chrono::milliseconds(100)) {
-                // not expected: take the launch path for this call and stop using the worker
+                // the generation is gone once stopped and its stream drained; a call it did not finish takes
+                // the launch path (its outcome is that path's status, so no error is recorded here)
                 (void)stop();
                 (void)hipStreamSynchronize(st);
-                broken = true;
-                set_last_error("call worker: a call did not complete within 100 ms; worker disabled");
-                return done(slot, s) ? 0 : 1;
+                back_off();
+                if (!done(slot, s)) return 1;
+                calls++;
+                return 0;
             }
             if (t - t0 > std::chrono::microseconds(200)) std::this_thread::yield();
             else __builtin_ia32_pause();
         }
         calls++;
+        timeouts_in_row = 0;
         return 0;
     }
 };
@@ -1602,7 +1770,7 @@ int call_worker_stats(long long* calls, long long* launches, long long* relaunch
     if (calls) *calls = w.calls;
     if (launches) *launches = w.launches;
     if (relaunches) *relaunches = w.relaunches;
-    if (disabled) *disabled = w.broken ? 1 : 0;
+    if (disabled) *disabled = (w.broken || w.cooling()) ? 1 : 0;
     return ECG_OK;
 }
 
@@ -1722,7 +1890,8 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
             const bool f = flagged && nflags + wg_max <= kFlagSlots;
             flagged = f;
             int posted = 0;
-            int rc = launch_one(op, dev.data(), B, st, /*latency=*/true, f ? c.flags_dev + nflags : nullptr, seq, &posted);
+            int rc = launch_one(op, dev.data(), B, st, /*host_tier=*/true, /*latency=*/true,
+                                f ? c.flags_dev + nflags : nullptr, seq, &posted);
             if (rc != ECG_OK) {
                 (void)hipStreamSynchronize(st);
                 return rc;
@@ -1764,7 +1933,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         }
     }
     for (const LinearOp& op : ops) {
-        int rc = launch_one(op, dev.data(), B, st);
+        int rc = launch_one(op, dev.data(), B, st, /*host_tier=*/true);
         if (rc != ECG_OK) {
             (void)hipStreamSynchronize(st);
             return rc;
@@ -1841,8 +2010,8 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
     a.binary = ps->binary ? 1 : 0;
     const bool vec_ok = aligned16(in_base) && aligned16(out_base) && (in_sstride % 16 == 0) &&
                         (in_bstride % 16 == 0) && (out_sstride % 16 == 0) && (out_bstride % 16 == 0);
-    ps->used_on(st);
     ECG_HIP(launch_gf(a, GF_MODE_STRIDED, vec_ok, st));
+    note_launch(*ps, st);
     return ECG_OK;
 }
 
@@ -1869,8 +2038,8 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
     a.MT = ps->MT;
     a.rtiles = ps->rtiles;
     a.binary = ps->binary ? 1 : 0;
-    ps->used_on(st);
     ECG_HIP(launch_gf(a, GF_MODE_PTRS, aligned, st));
+    note_launch(*ps, st);
     return ECG_OK;
 }
 
@@ -1927,7 +2096,6 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     std::shared_ptr<ProgramSet> ps = program_set(&dev, 1, &status, s_comp);
     if (!ps) return status;
     if (const int rc = ps->ensure_ready(s_comp); rc != ECG_OK) return rc;
-    ps->used_on(s_comp);
     const uint8_t* hin = (const uint8_t*)h_in;
     uint8_t* hout = (uint8_t*)h_out;
     const bool in_pinned = host_pinned(h_in), out_pinned = host_pinned(h_out);

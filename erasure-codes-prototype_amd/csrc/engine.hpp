@@ -46,23 +46,39 @@ struct ProgramSet {
     int* d_dst = nullptr;
     int nprog = 0, k = 0, m = 0, MT = 1, rtiles = 1;
     bool binary = false;
-    // streams the set's tables were launched on (for its retirement after eviction: a completion event
-    // per stream instead of a device-wide synchronize); more than kMaxStreams -> synchronize the device
+    // Retirement after eviction: the tables are freed only once every launch that reads them has completed.
+    // A caller stream is never handed to the runtime after the call that passed it returns -- the caller
+    // may destroy it, and the runtime crashes on a destroyed handle (hipEventRecord / hipStreamQuery
+    // segfault, profiles/r04/stream/) -- and no event is recorded per launch either (a separate
+    // hipEventRecord or a stop event bound to each launch cost ~3 us of host and GPU time per small launch,
+    // profiles/r04/stream/).  Instead a launch only notes its stream handle (compared, never passed to
+    // HIP).  Once the set is retired and nobody holds it, each noted stream gets a "cover" event recorded on
+    // it the next time the library is handed that stream anyway (a later launch or cache miss on it: the
+    // stream is alive then, and a record then follows every earlier launch on it).  The null stream and
+    // hipStreamPerThread are never destroyed, so they are covered at once.  A set whose streams are never
+    // seen again (destroyed, or idle) waits in a bounded graveyard, emptied by a device synchronize when it
+    // outgrows kGraveyardMax or on ecg_program_sets_reclaim.  Host-tier launches are not noted: those calls
+    // wait for their own completion before they return.  More than kMaxStreams streams -> graveyard.
     static constexpr int kMaxStreams = 8;
+    struct CoverEvent;
+    struct StreamSlot {
+        hipStream_t st;                     // compared, never passed to HIP
+        std::shared_ptr<CoverEvent> cover;  // recorded on st after the set was retired
+    };
     std::mutex smu;
-    hipStream_t streams[kMaxStreams] = {};
-    int nstreams = 0;
+    StreamSlot slots[kMaxStreams] = {};
+    int nslots = 0;
     bool overflow = false;
-    void used_on(hipStream_t s) {
+    void used_on(hipStream_t st) {  // launch path: note the caller stream
         std::lock_guard<std::mutex> lk(smu);
-        for (int i = 0; i < nstreams; i++)
-            if (streams[i] == s) return;
-        if (nstreams < kMaxStreams) streams[nstreams++] = s;
+        for (int i = 0; i < nslots; i++)
+            if (slots[i].st == st) return;
+        if (nslots < kMaxStreams) slots[nslots++].st = st;
         else overflow = true;
     }
     // upload state (program_set): the tables are copied on the first requesting stream
     hipEvent_t ready_ev = nullptr;
-    hipStream_t first_stream = nullptr;
+    hipStream_t first_stream = nullptr;  // compared only
     std::atomic<bool> ready{false};
     void* pinned = nullptr;  // source of the asynchronous upload (pinned pool block, returned once ready)
     size_t pinned_class = 0;
@@ -111,19 +127,44 @@ public:
 
     int launch_direct(const std::vector<LinearOp>& ops, uint8_t* const* blocks, long long B, hipStream_t stream);
 
+    // Events (retirement covers, batch-scope ordering), pooled.  acquire_event creates on the current
+    // device, which must be this engine's; release only an event no pending wait can still need recorded
+    // again (a wait already enqueued refers to the record at the time of the wait).
+    hipEvent_t acquire_event();
+    void release_event(hipEvent_t ev);
+
+    // After enqueueing a launch of `ps` on caller stream st (device and batched tiers): note the stream on
+    // the set and, if retired sets wait for a cover on a stream hashing like st, cover them on st now.
+    void note_launch(ProgramSet& ps, hipStream_t st) {
+        ps.used_on(st);
+        if (cover_mask_.load(std::memory_order_relaxed) & stream_bit(st)) cover_retired(st);
+    }
+    size_t retired_pending();  // evicted sets not yet freed (sweeps first; no synchronize)
+    size_t reclaim();          // synchronize the device, free every retired set nobody holds; pending after
+
 private:
     explicit Engine(int device);
     // latency: the blocks are host memory read over PCIe (zero-copy host tier) -> GF_MODE_INLINE_LAT
     // latency: the zero-copy host-tier variant; with flags (device view), it also posts completion flags
     // at flags[0, *n_flags) with value seq (GfLaunch::done_flags)
-    int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream, bool latency = false,
-                   unsigned* flags = nullptr, unsigned seq = 0, int* n_flags = nullptr);
+    // host_tier: `stream` is a leased host-tier stream and the call waits for the launch before it returns,
+    // so the launch is not noted for retirement (ProgramSet::used_on)
+    int launch_one(const LinearOp& op, uint8_t* const* blocks, long long B, hipStream_t stream, bool host_tier,
+                   bool latency = false, unsigned* flags = nullptr, unsigned seq = 0, int* n_flags = nullptr);
 
     // Evicted sets wait here until nothing can read their tables: first until no caller holds them (no
-    // further launch can be enqueued), then until a completion event recorded on every stream they were
-    // launched on has fired.  Swept on every cache miss; no device-wide synchronize on this path.
+    // further launch can be enqueued), then until the cover event of every stream they were launched on has
+    // fired (ProgramSet: covers are recorded on a stream only while the library holds it from a caller).
+    // Swept on every cache miss, with the miss's stream as `current`; no device-wide synchronize unless the
+    // graveyard of sets that cannot be covered outgrows kGraveyardMax.
+    static constexpr size_t kGraveyardMax = 16384;
     void retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted);
-    void sweep_retired();
+    void sweep_retired(hipStream_t current, bool has_current);
+    void cover_retired(hipStream_t st);  // a launch on st hit the cover mask
+    void sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead);
+    static uint64_t stream_bit(hipStream_t st) {
+        return 1ull << ((((uintptr_t)st >> 4) * 0x9E3779B97F4A7C15ull) >> 58);
+    }
     // Device memory of program tables comes from a pool of power-of-two blocks, so a steady stream of new
     // programs (a proxy's open set of repair matrices) neither allocates nor frees device memory --
     // hipFree synchronizes the device.  Uploads go through a private non-blocking stream.
@@ -143,19 +184,16 @@ private:
     std::mutex mu_;
     uint64_t tick_ = 0;
     std::unordered_map<std::string, CacheEntry> cache_;  // LRU-bounded by ECG_OPT_PROGRAM_CACHE
-    struct Retired {
-        std::shared_ptr<ProgramSet> ps;
-        std::vector<hipEvent_t> evs;
-        bool armed = false;
-    };
     std::mutex rmu_;
-    std::vector<Retired> retired_;
+    std::vector<std::shared_ptr<ProgramSet>> retired_;
+    // unheld retired sets waiting for a cover on each stream (rebuilt by every sweep; weak: the sets are
+    // owned by retired_), and the stream_bit of every stream in it
+    std::unordered_map<hipStream_t, std::vector<std::weak_ptr<ProgramSet>>> waiting_;
+    std::atomic<uint64_t> cover_mask_{0};
     std::mutex pmu_;
     std::unordered_map<size_t, std::vector<void*>> pool_, pinned_pool_;
+    std::vector<hipEvent_t> event_pool_;
     size_t pooled_bytes_ = 0, pinned_pooled_bytes_ = 0;
-
-public:
-    size_t retired_pending();  // evicted sets not yet freed (tests)
 };
 
 // Deferred-batch scope of the calling thread (ecg_batch_begin / ecg_batch_end).  Inside a scope,
@@ -331,7 +369,7 @@ std::vector<std::vector<size_t>> schedule_groups(size_t n, Key key, Reads reads,
 }
 
 // Resident call worker of the calling thread's device (ECG_OPT_CALL_WORKER): calls, launches, relaunches,
-// disabled after a failure.
+// off now (set-up failure, or a cooldown after a timed-out call).
 int call_worker_stats(long long* calls, long long* launches, long long* relaunches, int* disabled);
 
 // Last HIP error seen by this thread (for diagnostics through the C ABI).

@@ -566,15 +566,32 @@ void init_options() {
     g_opt_init.store(1, std::memory_order_release);
 }
 
-using Launcher = void (*)(const GfLaunch&, dim3, hipStream_t);
+// Launchers return the status of THEIR launch (hipLaunchKernel's return value): the thread's sticky
+// last error (hipGetLastError) also holds errors of earlier runtime calls the caller made and handled, and
+// the library neither reads nor clears that state.
+using Launcher = hipError_t (*)(const GfLaunch&, dim3, hipStream_t);
+
+template <typename T>
+struct NoDeduce {
+    using type = T;
+};
+
+template <typename... P>
+hipError_t launch_kernel(void (*kernel)(P...), dim3 grid, dim3 block, hipStream_t st,
+                         typename NoDeduce<P>::type... args) {
+    void* argv[] = {(void*)&args...};
+    return hipLaunchKernel((const void*)kernel, grid, block, argv, 0, st);
+}
 
 template <typename F>
-void launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL(kernel, grid, dim3(kThreads), 0, st, a);
+hipError_t launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
+    return launch_kernel(kernel, grid, dim3(kThreads), st, a);
 }
 
 template <int MT, int MODE, int NT, bool BIN>
-void gen_launch(const GfLaunch& a, dim3 g, hipStream_t st) { launch_with(gf_vec_kernel<MT, MODE, NT, BIN>, a, g, st); }
+hipError_t gen_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
+    return launch_with(gf_vec_kernel<MT, MODE, NT, BIN>, a, g, st);
+}
 
 template <int MODE, int NT, bool BIN>
 Launcher gen_pick(int MT) {
@@ -607,9 +624,9 @@ Launcher pick_vec(const GfLaunch& a, int nt) {
 }
 
 template <int MT, bool BIN, int KB>
-void lat_dword_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
-    if (a.B <= kLatEagerBytes) hipLaunchKernelGGL((gf_lat_dword_kernel<MT, BIN, KB, true>), g, dim3(kLatThreads), 0, st, a);
-    else hipLaunchKernelGGL((gf_lat_dword_kernel<MT, BIN, KB, false>), g, dim3(kLatThreads), 0, st, a);
+hipError_t lat_dword_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
+    if (a.B <= kLatEagerBytes) return launch_kernel(gf_lat_dword_kernel<MT, BIN, KB, true>, g, dim3(kLatThreads), st, a);
+    return launch_kernel(gf_lat_dword_kernel<MT, BIN, KB, false>, g, dim3(kLatThreads), st, a);
 }
 
 // input-count buckets of the latency kernel: exact for the BASELINE shapes (RS(6,4), RS(10,4) encode and
@@ -641,7 +658,9 @@ Launcher pick_lat_dword_bin(int MT, int k) {
 }
 
 template <int MT, int MODE, bool BIN>
-void byte_launch(const GfLaunch& a, dim3 g, hipStream_t st) { launch_with(gf_byte_kernel<MT, MODE, BIN>, a, g, st); }
+hipError_t byte_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
+    return launch_with(gf_byte_kernel<MT, MODE, BIN>, a, g, st);
+}
 
 template <int MODE, bool BIN>
 Launcher pick_byte_bin(int MT) {
@@ -705,10 +724,6 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         return hipErrorInvalidValue;
     if (base.B == 0) return hipSuccess;
     init_options();
-    // hipGetLastError after a launch names the thread's last error from ANY runtime call: clear what an
-    // earlier call left that its caller handled (e.g. the retirement's event on a stream the caller has
-    // destroyed since, which falls back to a device synchronize), so it is not taken for this launch's
-    (void)hipGetLastError();
     GfLaunch a = base;
     const long long vec_bytes = vec_ok ? (a.B & ~15LL) : 0;
     if (mode == GF_MODE_INLINE_LAT && vec_bytes == a.B && a.B <= g_opt[ECG_OPT_LAT_DWORD_BYTES].load() &&
@@ -717,8 +732,7 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         const long long gx = ((a.B >> 2) + kLatThreads - 1) / kLatThreads;
         Launcher l = a.binary ? pick_lat_dword_bin<true>(a.MT, a.k) : pick_lat_dword_bin<false>(a.MT, a.k);
         if (!l) return hipErrorInvalidValue;
-        l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
-        hipError_t e = hipGetLastError();
+        const hipError_t e = l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
         if (e != hipSuccess) return e;
         if (n_wg) *n_wg = (int)(gx * a.rtiles);
         return hipSuccess;
@@ -751,8 +765,7 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         }
         if (!l) return hipErrorInvalidValue;
         if (a.done_flags && (mode != GF_MODE_INLINE_LAT || vec_bytes < a.B)) return hipErrorInvalidValue;
-        l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
-        hipError_t e = hipGetLastError();
+        const hipError_t e = l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
         if (e != hipSuccess) return e;
         if (n_wg) *n_wg = (int)(gx * a.rtiles);
     }
@@ -776,8 +789,7 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
             default: return hipErrorInvalidValue;
         }
         if (!l) return hipErrorInvalidValue;
-        l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
-        hipError_t e = hipGetLastError();
+        const hipError_t e = l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -785,9 +797,7 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
 
 hipError_t launch_call_worker(const WorkerArgs& a, int workgroups, hipStream_t st) {
     if (workgroups < 1 || workgroups > kWorkerMaxWG) return hipErrorInvalidValue;
-    (void)hipGetLastError();  // a handled earlier error is not this launch's (launch_gf)
-    hipLaunchKernelGGL(gf_call_worker_kernel, dim3((unsigned)workgroups), dim3(kLatThreads), 0, st, a);
-    return hipGetLastError();
+    return launch_kernel(gf_call_worker_kernel, dim3((unsigned)workgroups), dim3(kLatThreads), st, a);
 }
 
 hipError_t launch_fill_splitmix(void* dst, long long nbytes, unsigned long long seed,
@@ -796,10 +806,8 @@ hipError_t launch_fill_splitmix(void* dst, long long nbytes, unsigned long long 
     const long long nwords = (nbytes + 7) >> 3;
     long long blocks = (nwords + kThreads - 1) / kThreads;
     if (blocks > 8192) blocks = 8192;
-    (void)hipGetLastError();  // a handled earlier error is not this launch's (launch_gf)
-    hipLaunchKernelGGL(fill_splitmix_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st,
-                       (uint8_t*)dst, nbytes, seed, word_offset);
-    return hipGetLastError();
+    return launch_kernel(fill_splitmix_kernel, dim3((unsigned)blocks), dim3(kThreads), st, (uint8_t*)dst, nbytes,
+                         seed, word_offset);
 }
 
 void make_coef_tab(int c, CoefTab* t) {

@@ -60,7 +60,7 @@ class RepairPlan:  # include/ec/erasure_code.h:53-58
 
 # Every symbol include/ecg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free", "ecg_program_cache_size", "ecg_program_sets_retiring", "ecg_host_contexts",
+    "ecg_last_error", "ecg_version", "ecg_device_count", "ecg_set_device", "ecg_free", "ecg_program_cache_size", "ecg_program_sets_retiring", "ecg_program_sets_reclaim", "ecg_host_contexts",
     "ecg_host_pinned_xfer_threshold", "ecg_call_worker_stats",
     "ecg_set_option", "ecg_get_option",
     "ecg_reed_sol_vandermonde_coding_matrix", "ecg_cauchy_good_general_coding_matrix",
@@ -152,6 +152,7 @@ def lib():
         "ecg_region_xor_batch": ([P, LL, P, LL, LL, I, P], I),
         "ecg_program_cache_size": ([], I),
         "ecg_program_sets_retiring": ([], I),
+        "ecg_program_sets_reclaim": ([], I),
         "ecg_host_contexts": ([], I),
         "ecg_host_pinned_xfer_threshold": ([], LL),
         "ecg_call_worker_stats": ([ctypes.POINTER(LL)] * 3 + [ctypes.POINTER(I)], I),

@@ -44,9 +44,16 @@ int ecg_device_count(void);
 int ecg_set_device(int device);    /* selects the HIP device for the calling thread */
 void ecg_free(void* p);            /* frees matrices returned by this library (malloc'd, like Jerasure) */
 int ecg_program_cache_size(void);  /* programs cached for the current device (diagnostics) */
-/* Evicted program tables of the current device not yet freed: each waits for its launches to complete
- * (a completion event per stream it ran on, never a device-wide synchronize).  Diagnostics. */
+/* Evicted program tables of the current device not yet freed (diagnostics).  An evicted set is freed once
+ * its launches have completed, proven by an event the library records on each stream the set ran on the
+ * next time a caller hands it that stream (the library never names a caller stream after the call that
+ * passed it returns: callers may destroy their streams at any time).  Sets whose streams are not seen again
+ * wait in a bounded graveyard, emptied by one device synchronize when it grows past 16384 sets, or by
+ * ecg_program_sets_reclaim. */
 int ecg_program_sets_retiring(void);
+/* Synchronize the current device and free every evicted program set no call still holds (e.g. at idle, or
+ * after a burst of per-request streams).  Returns the sets still retiring after it. */
+int ecg_program_sets_reclaim(void);
 /* Host-tier contexts (stream + device scratch + pinned staging) created so far for the current device
  * (diagnostics).  Contexts are pooled and leased per call, so this is bounded by the most host-tier calls
  * ever in flight at once, not by the number of threads that called (the reference's proxy starts a
@@ -54,7 +61,9 @@ int ecg_program_sets_retiring(void);
 int ecg_host_contexts(void);
 /* Resident call worker of the current device (ECG_OPT_CALL_WORKER), diagnostics: calls it completed,
  * kernel launches (generations started), generations relaunched under a waiting call, and whether it is
- * disabled after a failure (1) or not (0).  Any pointer may be NULL. */
+ * off right now (1) or not (0): off for good if it could not be set up, or for a cooldown (1 s, doubling per
+ * consecutive timeout up to 64 s) after a call did not complete within 100 ms; calls then take the launch
+ * path.  Any pointer may be NULL. */
 int ecg_call_worker_stats(long long* calls, long long* launches, long long* relaunches, int* disabled);
 /* The HIP runtime's pinned-transfer threshold for pageable host memory, in bytes, as this process runs
  * it: GPU_PINNED_MIN_XFER_SIZE (MiB) from the environment, default 1 MiB.  A pageable hipMemcpy of more

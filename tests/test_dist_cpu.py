@@ -153,7 +153,7 @@ def _ring_worker(rank, world, port, S, chunk, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,S,chunk", [(2, 5, 2), (3, 4, 4)])
+@pytest.mark.parametrize("world,S,chunk", [(2, 5, 2), (3, 4, 4), (8, 3, 2)])
 def test_ring_partial_repair(world, S, chunk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -191,7 +191,7 @@ def _exchange_worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 5])
+@pytest.mark.parametrize("world", [2, 3, 5, 8])
 def test_exchange_shifted_pairs(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -221,7 +221,7 @@ def test_ring_exchange_single_rank_and_shape_checks():
         D.pipelined_ring_repair(3, 0, None, None, a, b, r)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_bench_launcher_spawns_ranks(n):
     """`python bench.py --gpus N` outside torch.distributed starts N fresh rank processes itself (the
     driver's SCALE command) and relays rank 0's line with n_gpus = N.  --launch-check stops every rank

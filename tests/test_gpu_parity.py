@@ -706,10 +706,28 @@ def test_decode_batch_rotating_patterns(ecg, oracle, torch_cuda):
     patterns = [[e] for e in range(n)]
     pos = torch.arange(S, device="cuda", dtype=torch.int32) % n
     out = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
+    # the erased block of every stripe is saved, then POISONED: a decode that read it (or copied it) fails
+    sidx = torch.arange(S, device="cuda")
+    saved = stripes[sidx, sidx % n].clone()
+    stripes[sidx, sidx % n] = 0xA5
     ecg.decode_batch(k, m, M, 1, patterns, stripes, out=out, pattern_of_stripe=pos)
     torch.cuda.synchronize()
+    assert torch.equal(out[:, 0], saved)
+    # byte for byte against the oracle's decode of the poisoned stripe (erased block = output)
+    for s in (0, 5, 13, S - 1):
+        h = [x.copy() for x in stripes[s].cpu().numpy()]
+        assert oracle.jerasure_matrix_decode(k, m, M, 1, [s % n, -1], h[:k], h[k:], B) == 0
+        assert np.array_equal(out[s, 0].cpu().numpy(), h[s % n]), s
+    # the check can fail: a plan that READS the poisoned block gives other bytes.  Rebuilding e + 1 reads
+    # the first k surviving blocks, which include e whenever e is a data block (e < k)
+    shifted = [[(e + 1) % n] for e in range(n)]
+    bad = torch.empty_like(out)
+    ecg.decode_batch(k, m, M, 1, shifted, stripes, out=bad, pattern_of_stripe=pos)
+    torch.cuda.synchronize()
+    nxt = stripes[sidx, (sidx + 1) % n]
     for s in range(S):
-        assert torch.equal(out[s, 0], stripes[s, s % n]), s
+        assert torch.equal(bad[s, 0], nxt[s]) == (s % n >= k), s
+    stripes[sidx, sidx % n] = saved
     # in place, pairs of erasures, stripes padded (block stride > B)
     pad = torch.zeros((4, n, B + 48), dtype=torch.uint8, device="cuda")
     view = pad[:, :, :B]
@@ -782,16 +800,24 @@ def test_full_size_rs10_4_round_trip(ecg, oracle, torch_cuda):
     ecg.encode_batch(k, m, M, stripes[:, :k], stripes[:, k:])
     pos = (torch.arange(S, device="cuda", dtype=torch.int32) % n).contiguous()
     out = torch.empty((S, 1, B), dtype=torch.uint8, device="cuda")
-    ecg.decode_batch(k, m, M, 1, [[e] for e in range(n)], stripes, out=out, pattern_of_stripe=pos)
-    torch.cuda.synchronize()
-    idx = torch.arange(S, device="cuda") % n
-    expect = stripes[torch.arange(S, device="cuda"), idx]
-    assert torch.equal(out[:, 0], expect)
-    for s in (0, 1234, S - 1):
+    sidx = torch.arange(S, device="cuda")
+    idx = sidx % n
+    samples = (0, 1234, S - 1)
+    for s in samples:  # parities of sampled stripes against the oracle, before any block is poisoned
         h = stripes[s].cpu().numpy()
         ref = [np.zeros(B, np.uint8) for _ in range(m)]
         oracle.jerasure_matrix_encode_simd(k, m, M, [h[j] for j in range(k)], ref, B)
         assert same([h[k + i] for i in range(m)], ref), s
+    # the erased block (s mod 14) is saved, then poisoned in place: the decode must not read it
+    expect = stripes[sidx, idx].clone()
+    stripes[sidx, idx] = 0x5A
+    ecg.decode_batch(k, m, M, 1, [[e] for e in range(n)], stripes, out=out, pattern_of_stripe=pos)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, 0], expect)
+    for s in samples:  # the oracle decodes the same poisoned stripe to the same bytes
+        h = [x.copy() for x in stripes[s].cpu().numpy()]
+        assert oracle.jerasure_matrix_decode(k, m, M, 1, [s % n, -1], h[:k], h[k:], B) == 0
+        assert np.array_equal(out[s, 0].cpu().numpy(), h[s % n]), s
     del stripes, out, expect
     torch.cuda.empty_cache()
 

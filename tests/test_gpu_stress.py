@@ -149,8 +149,9 @@ def test_thread_per_request_resources_bounded(ecg, oracle):
 
 
 def test_eviction_does_not_stall_other_streams(ecg, oracle):
-    """Program-cache eviction retires the evicted tables with a completion event per stream they ran on;
-    it neither synchronizes the device nor frees device memory (hipFree would).  A second stream keeps
+    """Program-cache eviction retires the evicted tables with a cover event recorded on each stream they ran
+    on the next time a caller hands the library that stream (engine.hpp ProgramSet); it neither
+    synchronizes the device nor frees device memory (hipFree would).  A second stream keeps
     ~0.4 s of encodes queued while this thread makes 24 calls that each evict: they must take no longer
     than the same 24 launches with their programs already cached (the control; streams can share one of
     the runtime's hardware queues, GPU_MAX_HW_QUEUES = 4, and then both wait alike), and every evicted set
@@ -195,6 +196,7 @@ def test_eviction_does_not_stall_other_streams(ecg, oracle):
             return dt
 
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 4096)
+        assert ecg.lib().ecg_program_sets_reclaim() == 0  # earlier tests' sets whose streams are gone
         timed_calls()  # programs built and cached
         control = timed_calls()  # the same launches, no eviction
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 2)
@@ -213,6 +215,99 @@ def test_eviction_does_not_stall_other_streams(ecg, oracle):
             oracle.jerasure_matrix_encode(4, 2, Mi, [host[j] for j in range(4)], want, Bs)
             assert np.array_equal(out.cpu().numpy(), np.stack(want))
         torch.cuda.synchronize()
-        assert ecg.lib().ecg_program_sets_retiring() == 0
+        # sets used on `mine` were covered by later calls on it; the encode's set, evicted by `mine`'s calls,
+        # waits for `busy` to be handed over again -- one more call on it frees it without any synchronize
+        ecg.encode_batch(k, m, M, big[:, :k], big[:, k:], stream=busy.cuda_stream)
+        ecg.dev_matrix_encode(4, 2, mats[0], [blocks[j] for j in range(4)], [outs[0][0], outs[0][1]], Bs,
+                              stream=mine.cuda_stream)
+        torch.cuda.synchronize()
+        left = ecg.lib().ecg_program_sets_retiring()
+        assert left <= 2, left  # at most the sets of the last two calls, still current
+        assert ecg.lib().ecg_program_sets_reclaim() == 0
+    finally:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
+
+
+def _hip():
+    """The HIP runtime torch loaded (same soname as libecg's), for raw caller streams."""
+    import ctypes
+    h = ctypes.CDLL("libamdhip64.so.7")
+    h.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    h.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    return h
+
+
+def test_eviction_retires_across_destroyed_and_reused_streams(ecg, oracle):
+    """The reference runs each EC call on a detached thread (proxy.cpp:416-419); an integrator with a stream
+    per request creates and DESTROYS raw HIP streams.  The runtime hands a destroyed handle to the next
+    hipStreamCreate, so a stored handle may name a dead stream or an unrelated new one.  Program sets used
+    on such streams are evicted (cache of 2) by calls on other streams; nothing the library keeps may name
+    a caller stream after the call returns, and every result is checked against the oracle.  Round 3
+    crashed here (gpurun_out/evict.log)."""
+    import ctypes
+
+    import torch
+    bt = os.path.join(os.path.dirname(os.path.abspath(__file__)), "segv", "libsegv_bt.so")
+    if os.path.exists(bt):  # native backtrace if anything below crashes (test helper, not product)
+        ctypes.CDLL(bt).segv_bt_install()
+    hip = _hip()
+    saved = ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE)
+    rng = np.random.default_rng(11)
+    Bs = 4096
+    blocks = torch.from_numpy(rng.integers(0, 256, (4, Bs), dtype=np.uint8)).cuda()
+    host = blocks.cpu().numpy()
+    mats = [[int(x) for x in rng.integers(1, 256, 4 * 2)] for _ in range(40)]
+    outs = [torch.zeros((2, Bs), dtype=torch.uint8, device="cuda") for _ in mats]
+    big = torch.empty((64, 14, 1 << 20), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(big, 0x5EED)
+    M = ecg.reed_sol_vandermonde_coding_matrix(10, 4)
+    torch.cuda.synchronize()
+    handles = []
+    try:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 2)
+        it = iter(zip(mats, outs))
+        for rnd in range(6):
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            handles.append(s.value)
+            # work queued on the caller stream, then calls whose program sets remember it
+            ecg.encode_batch(10, 4, M, big[:, :10], big[:, 10:], stream=s.value)
+            with ecg.batch():  # a scope on the caller stream (its flush orders after earlier flushes)
+                for _ in range(2):
+                    Mi, out = next(it)
+                    ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs,
+                                          stream=s.value)
+            for _ in range(2):
+                Mi, out = next(it)
+                ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs,
+                                      stream=s.value)
+            if rnd % 2 == 0:  # destroyed with its work still queued (hipStreamDestroy waits for it)
+                assert hip.hipStreamDestroy(s) == 0
+            else:  # or idle, and a new stream (often the same handle) created before the evicting calls
+                torch.cuda.synchronize()
+                assert hip.hipStreamDestroy(s) == 0
+                s2 = ctypes.c_void_p()
+                assert hip.hipStreamCreate(ctypes.byref(s2)) == 0
+                Mi, out = next(it)
+                ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs,
+                                      stream=s2.value)
+                hip.hipStreamSynchronize(s2)
+                assert hip.hipStreamDestroy(s2) == 0
+            # evicting calls on torch's stream: every set used on the dead stream is retired here
+            for _ in range(2):
+                Mi, out = next(it)
+                assert ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]],
+                                             Bs) == 0
+        torch.cuda.synchronize()
+        left = ecg.lib().ecg_program_sets_retiring()
+        print(f"stream handles {[hex(h) for h in handles]} ({len(set(handles))} distinct); "
+              f"{left} evicted sets wait for a stream not seen again")
+        used = len(mats) - sum(1 for _ in it)
+        for Mi, out in list(zip(mats, outs))[:used]:
+            want = [np.zeros(Bs, np.uint8) for _ in range(2)]
+            oracle.jerasure_matrix_encode(4, 2, Mi, [host[j] for j in range(4)], want, Bs)
+            assert np.array_equal(out.cpu().numpy(), np.stack(want))
+        # the sets whose last stream was destroyed are freed by a reclaim (device synchronize), nothing else
+        assert ecg.lib().ecg_program_sets_reclaim() == 0
     finally:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)

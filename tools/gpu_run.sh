@@ -1,0 +1,99 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-round tools/gpu_r0N_*.sh scripts).
+#   OUT=<dir under gpurun_out/> bash tools/gpu_run.sh STEP [STEP ...]
+# Steps, each under its own time limit; the run stops at the first step that fails:
+#   tests      GPU parity suite (-m gpu, one process, per-test thread timeout)  -> pytest_gpu.log
+#   test:<k>   GPU tests matching -k <k>                                          -> pytest_<k>.log
+#   smoke      __graft_entry__.smoke()                                            -> smoke.log
+#   bench      default bench line (python bench.py)                               -> bench.log
+#   headline   bench line of the headline alone (no config 5 / ring / host path)  -> bench_headline.log
+#   prof       rocprofv3 --kernel-trace --stats of the default line and of the headline alone
+#   pmc        FETCH_SIZE and WRITE_SIZE passes of the headline -> pmc_traffic.json (tools/parse_pmc.py)
+#   rehearsal  bench.py --gpus 2 on the one GPU (tools/gpu_dist_rehearsal.sh)
+#   rehearsal8 bench.py --gpus 8 on the one GPU, scaled down (tools/gpu_dist_rehearsal.sh, N=8)
+#   workloads  every bench.py --workload line                                    -> bench_<w>.log
+#   wprof      rocprofv3 kernel stats of each non-default workload
+#   w:<name>   one workload line                                                  -> bench_<name>.log
+#   wp:<name>  rocprofv3 kernel stats of one workload
+#   callrate   tools/call_rate + tools/record_cost (device-tier per-call cost)     -> call_rate.txt, record_cost.txt
+#   ab         per-call cost A/B: the tree's libecg vs erasure-codes-prototype_amd/lib/ab/ (a build of an earlier
+#              commit), tools/call_rate device + tools/record_cost, alternated over 3 rounds -> ab_<v>_<r>.txt
+set -u
+cd "$GRAFT_REPO_ROOT"
+R=$GRAFT_REPO_ROOT
+O=gpurun_out/${OUT:-run}
+mkdir -p "$O"
+PYT="python -u -m pytest -p no:cacheprovider --timeout 120 --timeout-method thread"
+HEADLINE="--no-config5 --no-ring --no-host-path"
+
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@"
+  local rc=$?
+  echo "$name rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+}
+
+prof() {  # dir log args...
+  local d=$1 log=$2; shift 2
+  (cd /tmp && TMPDIR=/tmp timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$R/$O/$d" -o run --output-format csv \
+     -- python3 "$R/bench.py" "$@" > "$R/$O/$log" 2>&1)
+  local rc=$?
+  echo "rocprof $d rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+}
+
+pmc() {  # counter tag
+  (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc "$1" -d "$R/$O/pmc_$2" -o "$2" --output-format csv \
+     -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline $HEADLINE > "$R/$O/pmc_$2.log" 2>&1)
+  local rc=$?
+  echo "pmc $1 rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+}
+
+WORKLOADS="rs-decode-patterns lrc-repair pc-merge rs4m-waves rs-host"
+RINGS="lrc-repair-ring lrc-global-ring pc-merge-ring"
+
+for step in "$@"; do
+  case $step in
+    tests) run tests 1200 $PYT tests -q -m gpu > "$O/pytest_gpu.log" 2>&1 || true
+           grep -E "^(FAILED|ERROR)|passed|failed" "$O/pytest_gpu.log" | tail -8 ;;
+    test:*) k=${step#test:}
+           run "test $k" 600 $PYT tests -v -s -m gpu -k "$k" > "$O/pytest_${k// /_}.log" 2>&1 || true
+           tail -3 "$O/pytest_${k// /_}.log" ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1; tail -1 "$O/smoke.log" ;;
+    bench) run bench 500 python bench.py > "$O/bench.log" 2>&1; tail -1 "$O/bench.log" | cut -c1-400 ;;
+    headline) run headline 400 python bench.py --no-cpu-baseline $HEADLINE > "$O/bench_headline.log" 2>&1
+           tail -1 "$O/bench_headline.log" | cut -c1-400 ;;
+    prof) prof prof prof.log --steps 40 --warmup 3 --no-cpu-baseline
+          prof prof_headline prof_headline.log --steps 40 --warmup 3 --no-cpu-baseline $HEADLINE ;;
+    pmc) pmc FETCH_SIZE fetch; pmc WRITE_SIZE write
+         python tools/parse_pmc.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" \
+           "$O/pmc_traffic.json" rs104_B1048576_S4096 > /dev/null && echo "pmc parse ok" || exit 1 ;;
+    rehearsal) run rehearsal 600 bash tools/gpu_dist_rehearsal.sh > "$O/rehearsal.log" 2>&1; tail -3 "$O/rehearsal.log" ;;
+    rehearsal8) N=8 run rehearsal8 900 bash tools/gpu_dist_rehearsal.sh > "$O/rehearsal8.log" 2>&1; tail -3 "$O/rehearsal8.log" ;;
+    workloads) for w in $WORKLOADS; do
+                 run "bench $w" 500 python bench.py --workload $w --no-cpu-baseline > "$O/bench_$w.log" 2>&1
+               done
+               for w in $RINGS; do
+                 run "bench $w" 300 python bench.py --workload $w --self-p2p > "$O/bench_$w.log" 2>&1
+               done ;;
+    wprof) for w in rs-decode-patterns lrc-repair pc-merge rs4m-waves; do
+             prof "wprof/$w" "wprof_$w.log" --workload $w --no-cpu-baseline
+           done ;;
+    w:*) w=${step#w:}; run "bench $w" 500 python bench.py --workload $w --no-cpu-baseline > "$O/bench_$w.log" 2>&1
+         tail -1 "$O/bench_$w.log" | cut -c1-600 ;;
+    wp:*) w=${step#wp:}; prof "wprof/$w" "wprof_$w.log" --workload $w --no-cpu-baseline ;;
+    callrate) run call_rate 300 ./tools/call_rate > "$O/call_rate.txt" 2>&1
+              run record_cost 300 ./tools/record_cost > "$O/record_cost.txt" 2>&1 ;;
+    ab) for r in 1 2 3; do
+          for v in new prev; do
+            if [ $v = prev ]; then LP=$R/erasure-codes-prototype_amd/lib/ab; else LP=$R/erasure-codes-prototype_amd/lib; fi
+            LD_LIBRARY_PATH=$LP run "call_rate $v $r" 200 ./tools/call_rate 3 device > "$O/ab_${v}_$r.txt" 2>&1
+            LD_LIBRARY_PATH=$LP run "record_cost $v $r" 200 ./tools/record_cost >> "$O/ab_${v}_$r.txt" 2>&1
+          done
+        done
+        grep -H -E "dev_matrix|record " "$O"/ab_*.txt | cut -c1-160 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
