@@ -62,6 +62,7 @@ from ecg_ring import (azure_local_split, global_ring_state, pc_merge_ring_state,
                       ring_repair_state)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+REPLAY_THREADS = (4, 8, 16)  # lrc-repair: concurrent host threads issuing the per-call reference sequence
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 METRIC = "GiB/s encode + single-block decode (device-resident), RS(10,4) 1 MiB blocks, 1 & 8 GPU"
 # BASELINE.json configs[4]: RS(10,4), 4 MiB blocks, 65536 stripes sharded over the GPUs, encoded in
@@ -85,6 +86,8 @@ def parse():
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
     ap.add_argument("--chunk", type=int, default=None, help="lrc-repair-ring: stripes per transfer")
+    ap.add_argument("--forms", default=None,
+                    help="lrc-repair: comma-separated subset of its forms (default: all), e.g. for a profile")
     ap.add_argument("--self-p2p", action="store_true",
                     help="lrc-repair-ring at N = 1: rank 0 sends the partials to itself over RCCL point to point "
                          "(the N > 1 nccl code path on one GPU; the rate is an intra-GPU copy, not xGMI)")
@@ -190,6 +193,34 @@ def timed_loop(r, steps, step):
     D.barrier(r)
     elapsed = time.perf_counter() - t0
     return D.max_over_ranks(elapsed, r, device="cuda"), evs
+
+
+PROFILE_FILE = os.path.join(ROOT, "profiles", "headline_profile.json")
+
+
+def libecg_sha16():
+    import hashlib
+    with open(os.path.join(ROOT, "erasure-codes-prototype_amd", "lib", "libecg.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def committed_profile():
+    """The committed headline-only rocprofv3 summary (tools/profile_summary.py) and PMC file, named beside
+    this run's HIP-event fractions, with whether they were taken on this very libecg.so build."""
+    out = {}
+    try:
+        prof = json.load(open(PROFILE_FILE))
+        me = libecg_sha16()
+        out = {"profile_kernel_avg_ms": prof["encode"]["avg_ms"], "profile_frac": prof["encode"]["frac_avg"],
+               "profile_decode_avg_ms": prof["decode"]["avg_ms"], "profile_decode_frac": prof["decode"]["frac_avg"],
+               "profile_source": "profiles/headline_profile.json <- " + prof["source"],
+               "profile_libecg_sha16": prof["libecg_sha16"], "profile_is_this_build": prof["libecg_sha16"] == me}
+        pm = json.load(open(PMC_FILE))
+        out["traffic_libecg_sha16"] = pm.get("libecg_sha16")
+        out["traffic_is_this_build"] = pm.get("libecg_sha16") == me
+    except Exception:  # noqa: BLE001 -- no committed profile: the line says so
+        out.setdefault("profile_source", None)
+    return out
 
 
 def pmc_traffic(tag, workload_key):
@@ -373,7 +404,9 @@ def rs_encode_decode(a, r):
                      "algorithmic_bytes_per_launch": enc_bytes,
                      "decode_achieved": round(dec_bytes / dec_avg / 1e9, 1),
                      "decode_frac": round(dec_bytes / dec_avg / 1e9 / HBM_PEAK_GBS, 4),
-                     "decode_traffic": pmc_traffic("decode", f"rs{k}{m}_B{B}_S{S}")},
+                     "decode_traffic": pmc_traffic("decode", f"rs{k}{m}_B{B}_S{S}"),
+                     "frac_source": "HIP events on this run's stream, averaged over the timed steps",
+                     **committed_profile()},
         "parity_checksums": [f"{c:016x}" for c in checks],
     }
     # every rank's own kernel times and HBM fractions (HIP events on its stream), not rank 0's only
@@ -601,6 +634,39 @@ def lrc_repair(a, r):
                 ev[1].record()
         return fn
 
+    def replay_threads(nthreads):
+        """The per-call sequence (form 0) from `nthreads` concurrent host threads, each with its own
+        ErasureCode handle and stream over a contiguous share of the repairs (the proxy's thread per
+        request, proxy.cpp:416-419).  The worker streams start after and finish before the current stream's
+        events, so the events time the whole."""
+        import ctypes
+        ecs = [ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp) for _ in range(nthreads)]
+        for e in ecs:
+            e.init_coding_parameters(cp)
+        streams = [torch.cuda.Stream() for _ in range(nthreads)]
+        ec_arr = (ctypes.c_void_p * nthreads)(*[e._h for e in ecs])
+        st_arr = (ctypes.c_void_p * nthreads)(*[s.cuda_stream for s in streams])
+
+        def fn(ev=None):
+            cur = torch.cuda.current_stream()
+            if ev:
+                ev[0].record()
+            for s_ in streams:
+                s_.wait_stream(cur)
+            rc = rp.ecg_replay_partial_repair_mt(
+                ec_arr, st_arr, nthreads, 0, scope_stripes, stripes.data_ptr(), stripes.stride(0), stripes.stride(1), B,
+                sl.numel(), sl_h.data_ptr(), pl_h.data_ptr(), fail_h.data_ptr(), 6, surv_h.data_ptr(), 3,
+                help_h.data_ptr(), 3, main_h.data_ptr(), part_scratch.data_ptr(), rebuilt.data_ptr(), rebuilt.stride(0))
+            if rc != 0:
+                raise ecg.EcgError(rc, "ecg_replay_partial_repair_mt")
+            for s_ in streams:
+                cur.wait_stream(s_)
+            ecg.matrix_apply_batch_multi(glob_progs, stripes, rebuilt, prog_of_stripe=pg, stripe_of=sg)
+            if ev:
+                ev[1].record()
+        fn.keep = (ecs, streams, ec_arr, st_arr)
+        return fn
+
     idx = torch.arange(S, device="cuda")
     results = {}
     n_local, n_glob = sl.numel(), sg.numel()
@@ -610,7 +676,11 @@ def lrc_repair(a, r):
              ("fused", step_fused, alg),
              ("reference_sequence_per_call", replay(0), (n_local * (4 + 4 + 3) + n_glob * 13) * B),
              ("reference_sequence_scope", replay(1), (n_local * (4 + 4 + 3) + n_glob * 13) * B),
-             ("reference_sequence_scope_scratch", replay(2), None))
+             ("reference_sequence_scope_scratch", replay(2), None),
+             *((f"reference_sequence_per_call_threads{t}", replay_threads(t),
+                (n_local * (4 + 4 + 3) + n_glob * 13) * B) for t in REPLAY_THREADS))
+    if a.forms:
+        forms = tuple(f for f in forms if f[0] in a.forms.split(","))
     for name, fn, executed in forms:
         rebuilt.zero_()
         for _ in range(a.warmup):
@@ -632,6 +702,9 @@ def lrc_repair(a, r):
             res["last_scope_flush"] = replay_stats[1]
         if name.startswith("reference_sequence"):
             res["issued_from"] = "C++ through the C ABI (loopback/replay.cpp), one ErasureCode call per step per stripe"
+        if "_threads" in name:
+            res["issued_from"] += (f"; {name.rsplit('threads', 1)[1]} host threads, each with its own handle and "
+                                   "stream over a contiguous share of the repairs")
         res["executed_bytes_per_batch"] = executed
         res["executed_GBps"] = round(executed / t / 1e9, 1) if executed else None
         results[name] = res
@@ -655,6 +728,8 @@ def replay_lib():
         I, LL, P = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p
         L.ecg_replay_partial_repair.argtypes = [P, I, I, P, LL, LL, I, I, P, P, P, I, P, I, P, I, P, P, P, LL, P]
         L.ecg_replay_partial_repair.restype = I
+        L.ecg_replay_partial_repair_mt.argtypes = [P, P, I, I, I, P, LL, LL, I, I, P, P, P, I, P, I, P, I, P, P, P, LL]
+        L.ecg_replay_partial_repair_mt.restype = I
         _REPLAY = L
     return _REPLAY
 

@@ -32,7 +32,7 @@ thread_local std::string t_last_error;
 
 constexpr int kMaxDevices = 64;
 std::mutex g_engines_mu;
-Engine* g_engines[kMaxDevices] = {};
+std::atomic<Engine*> g_engines[kMaxDevices] = {};
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
@@ -407,9 +407,11 @@ Engine& Engine::instance() {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= kMaxDevices) dev = 0;
+    if (Engine* e = g_engines[dev].load(std::memory_order_acquire)) return *e;  // every call: no lock
     std::lock_guard<std::mutex> lk(g_engines_mu);
-    if (!g_engines[dev]) g_engines[dev] = new Engine(dev);  // lives for the process
-    return *g_engines[dev];
+    if (!g_engines[dev].load(std::memory_order_relaxed))
+        g_engines[dev].store(new Engine(dev), std::memory_order_release);  // lives for the process
+    return *g_engines[dev].load(std::memory_order_relaxed);
 }
 
 int Engine::host_contexts() const {
@@ -418,7 +420,7 @@ int Engine::host_contexts() const {
 }
 
 size_t Engine::cache_size() {
-    std::lock_guard<std::mutex> lk(mu_);
+    std::shared_lock<std::shared_mutex> lk(mu_);
     return cache_.size();
 }
 
@@ -458,10 +460,10 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
         binary &= op_is_binary(op);
     }
     {
-        std::lock_guard<std::mutex> lk(mu_);
+        std::shared_lock<std::shared_mutex> lk(mu_);
         auto it = cache_.find(key);
         if (it != cache_.end()) {
-            it->second.last_use = ++tick_;
+            it->second.last_use->store(tick_.fetch_add(1, std::memory_order_relaxed) + 1, std::memory_order_relaxed);
             return it->second.ps;
         }
     }
@@ -528,22 +530,22 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
     }
     std::vector<std::shared_ptr<ProgramSet>> evicted;  // retired outside the lock
     {
-        std::lock_guard<std::mutex> lk(mu_);
+        std::unique_lock<std::shared_mutex> lk(mu_);
         auto it = cache_.find(key);
         if (it != cache_.end()) {  // another thread won the race
-            it->second.last_use = ++tick_;
+            it->second.last_use->store(++tick_, std::memory_order_relaxed);
             return it->second.ps;
         }
         const size_t cap = (size_t)std::max(2LL, get_option(ECG_OPT_PROGRAM_CACHE));
         if (cache_.size() >= cap) {  // keep the cap / 2 most recently used programs
             std::vector<uint64_t> uses;
             uses.reserve(cache_.size());
-            for (auto& kv : cache_) uses.push_back(kv.second.last_use);
+            for (auto& kv : cache_) uses.push_back(kv.second.last_use->load(std::memory_order_relaxed));
             const size_t drop = cache_.size() - cap / 2;
             std::nth_element(uses.begin(), uses.begin() + drop, uses.end());
             const uint64_t cut = uses[drop];
             for (auto i = cache_.begin(); i != cache_.end();) {
-                if (i->second.last_use < cut) {
+                if (i->second.last_use->load(std::memory_order_relaxed) < cut) {
                     evicted.push_back(std::move(i->second.ps));
                     i = cache_.erase(i);
                 } else {
@@ -551,7 +553,7 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
                 }
             }
         }
-        cache_.emplace(key, CacheEntry{ps, ++tick_});
+        cache_.emplace(key, CacheEntry{ps, std::make_unique<std::atomic<uint64_t>>(++tick_)});
     }
     if (!evicted.empty()) retire(std::move(evicted));
     sweep_retired(st, true);  // st: the caller's stream, alive for this call

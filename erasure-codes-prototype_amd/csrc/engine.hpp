@@ -20,6 +20,7 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -69,12 +70,20 @@ struct ProgramSet {
     StreamSlot slots[kMaxStreams] = {};
     int nslots = 0;
     bool overflow = false;
+    std::atomic<int> nslots_pub{0};  // slots[0, nslots_pub) have their stream set (lock-free launch check)
     void used_on(hipStream_t st) {  // launch path: note the caller stream
+        const int n = nslots_pub.load(std::memory_order_acquire);
+        for (int i = 0; i < n; i++)
+            if (slots[i].st == st) return;  // the common case: no lock
         std::lock_guard<std::mutex> lk(smu);
         for (int i = 0; i < nslots; i++)
             if (slots[i].st == st) return;
-        if (nslots < kMaxStreams) slots[nslots++].st = st;
-        else overflow = true;
+        if (nslots < kMaxStreams) {
+            slots[nslots++].st = st;
+            nslots_pub.store(nslots, std::memory_order_release);
+        } else {
+            overflow = true;
+        }
     }
     // upload state (program_set): the tables are copied on the first requesting stream
     hipEvent_t ready_ev = nullptr;
@@ -179,10 +188,11 @@ private:
     int device_;
     struct CacheEntry {
         std::shared_ptr<ProgramSet> ps;
-        uint64_t last_use;
+        std::unique_ptr<std::atomic<uint64_t>> last_use;  // updated under the shared lock
     };
-    std::mutex mu_;
-    uint64_t tick_ = 0;
+    // hits (every launch) take the lock shared; builds and evictions take it exclusively
+    std::shared_mutex mu_;
+    std::atomic<uint64_t> tick_{0};
     std::unordered_map<std::string, CacheEntry> cache_;  // LRU-bounded by ECG_OPT_PROGRAM_CACHE
     std::mutex rmu_;
     std::vector<std::shared_ptr<ProgramSet>> retired_;

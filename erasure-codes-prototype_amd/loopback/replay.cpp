@@ -12,6 +12,7 @@
 //   2 scratch  the same scopes with the partial buffers declared scratch (ecg_batch_scratch): the three
 //              calls of a repair compose into one region product and the partials never reach HBM.
 // Not part of libecg (the product); a caller of it, like loopback/.
+#include <thread>
 #include <vector>
 
 #include "../../include/ecg.h"
@@ -68,6 +69,33 @@ int ecg_replay_partial_repair(ecg_ec* ec, int form, int scope_stripes, char* bas
         if (rc) return rc;
         if (re) return re;
     }
+    return 0;
+}
+
+// The same per-call sequence issued CONCURRENTLY, as the proxy issues it: the reference runs every request
+// on its own detached thread (proxy.cpp:416-419; handle_repair.cpp:246-252,370-376 per repair).  Thread t
+// takes the contiguous share [t S / n, (t + 1) S / n) of the repairs with its own ErasureCode handle ecs[t]
+// and its own stream streams[t]; threads are joined before returning (their launches stay asynchronous).
+int ecg_replay_partial_repair_mt(ecg_ec** ecs, void** streams, int nthreads, int form, int scope_stripes, char* base,
+                                 long long sstride, long long bstride, int B, int S, const int* stripe_of,
+                                 const int* pattern_of, const int* fail, int n_surv, const int* surv, int n_help,
+                                 const int* help, int n_main, const int* main_, char* partials, char* out,
+                                 long long out_stride) {
+    if (!ecs || !streams || nthreads < 1 || S < 0) return ECG_EINVAL;
+    std::vector<int> rcs(nthreads, 0);
+    std::vector<std::thread> th;
+    th.reserve(nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        const int c0 = (int)((long long)S * t / nthreads), c1 = (int)((long long)S * (t + 1) / nthreads);
+        th.emplace_back([=, &rcs] {
+            rcs[t] = ecg_replay_partial_repair(ecs[t], form, scope_stripes, base, sstride, bstride, B, c1 - c0,
+                                               stripe_of + c0, pattern_of + c0, fail, n_surv, surv, n_help, help,
+                                               n_main, main_, partials + 2LL * c0 * B, out, out_stride, streams[t]);
+        });
+    }
+    for (auto& x : th) x.join();
+    for (int rc : rcs)
+        if (rc) return rc;
     return 0;
 }
 

@@ -177,7 +177,10 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
  * group and of all later groups are discarded (the scope stays open, empty).  Scopes do not nest
  * (ECG_EINVAL).  While no scratch is declared (ecg_batch_scratch), the scope also flushes by itself
  * every 1024 recorded calls, so the GPU runs the first calls while the host records the rest; with
- * scratch declared, only every 65536 calls.  Declare scratch before recording the calls it is for. */
+ * scratch declared, only every 65536 calls.  Declare scratch before recording the calls it is for.
+ * Streams: a stream named by a recorded call must stay alive until the flush that launches the call
+ * (the launch goes onto it).  After a flush returns, the library does not name its streams again, so a
+ * caller may destroy them at once (ordering into the next flush uses an event recorded before return). */
 int ecg_batch_begin(void);
 int ecg_batch_flush(void);
 int ecg_batch_end(void);
@@ -272,6 +275,9 @@ ecg_ec* ecg_ec_factory(int ec_type, const ecg_coding_parameters* cp); /* metadat
 void ecg_ec_destroy(ecg_ec* ec);
 int ecg_ec_init_coding_parameters(ecg_ec* ec, const ecg_coding_parameters* cp);
 int ecg_ec_get_coding_parameters(ecg_ec* ec, ecg_coding_parameters* cp);
+/* ECG_MEM_DEVICE: later calls on the handle launch on `stream`.  The handle stores it, so the stream must
+ * stay alive while the handle's calls use it; the library itself never names it after a call returns
+ * (evicted program sets are retired without it; see ecg_program_sets_retiring). */
 int ecg_ec_set_memory(ecg_ec* ec, int mem, void* stream);
 int ecg_ec_set_isvertical(ecg_ec* ec, int isvertical); /* HPC::isvertical (pc.h:66) */
 int ecg_ec_k(const ecg_ec* ec);

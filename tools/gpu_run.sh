@@ -9,6 +9,8 @@
 #   headline   bench line of the headline alone (no config 5 / ring / host path)  -> bench_headline.log
 #   prof       rocprofv3 --kernel-trace --stats of the default line and of the headline alone
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the headline -> pmc_traffic.json (tools/parse_pmc.py)
+#   summary    tools/profile_summary.py over prof_headline's trace + pmc_traffic.json -> headline_profile.json
+#              (copy it and pmc_traffic.json to profiles/ to have bench.py's roofline name them)
 #   rehearsal  bench.py --gpus 2 on the one GPU (tools/gpu_dist_rehearsal.sh)
 #   rehearsal8 bench.py --gpus 8 on the one GPU, scaled down (tools/gpu_dist_rehearsal.sh, N=8)
 #   workloads  every bench.py --workload line                                    -> bench_<w>.log
@@ -70,6 +72,8 @@ for step in "$@"; do
     pmc) pmc FETCH_SIZE fetch; pmc WRITE_SIZE write
          python tools/parse_pmc.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" \
            "$O/pmc_traffic.json" rs104_B1048576_S4096 > /dev/null && echo "pmc parse ok" || exit 1 ;;
+    summary) python tools/profile_summary.py "$O/prof_headline/run_kernel_trace.csv" "$O/pmc_traffic.json" \
+               "$O/headline_profile.json" 40 > /dev/null && echo "summary ok" || exit 1 ;;
     rehearsal) run rehearsal 600 bash tools/gpu_dist_rehearsal.sh > "$O/rehearsal.log" 2>&1; tail -3 "$O/rehearsal.log" ;;
     rehearsal8) N=8 run rehearsal8 900 bash tools/gpu_dist_rehearsal.sh > "$O/rehearsal8.log" 2>&1; tail -3 "$O/rehearsal8.log" ;;
     workloads) for w in $WORKLOADS; do

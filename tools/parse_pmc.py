@@ -27,8 +27,13 @@ def load(pattern):
 def main(fetch_glob, write_glob, out, workload):
     f, fn = load(fetch_glob)
     w, wn = load(write_glob)
+    import hashlib
+    import os
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "erasure-codes-prototype_amd",
+                       "lib", "libecg.so")
     res = {"workload": workload, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
-           "correction": "FETCH_SIZE x2 (gfx950 half-count of 16-B/lane streaming reads); WRITE_SIZE as is; KiB -> B"}
+           "correction": "FETCH_SIZE x2 (gfx950 half-count of 16-B/lane streaming reads); WRITE_SIZE as is; KiB -> B",
+           "libecg_sha16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib) else None}
     for tag, key in (("encode", "gf_vec_kernel<4,"), ("decode", "gf_vec_kernel<1,")):
         fv = [v for d, v in f.items() if key in fn[d].replace(" ", "")]
         wv = [v for d, v in w.items() if key in wn[d].replace(" ", "")]
