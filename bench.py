@@ -958,9 +958,20 @@ def pc_merge(a, r):
     rows = [([[1] * 8], src[8 * row:8 * row + 8], [row]) for row in range(5)]
     prog_of = (torch.arange(5 * S, device="cuda", dtype=torch.int32) % 5).contiguous()
     stripe_of = (torch.arange(5 * S, device="cuda", dtype=torch.int32) // 5).contiguous()
+    def unsplit():  # the fused program as one 40-input launch stripe per merge (ECG_OPT_ROW_SPLIT = 0)
+        saved = ecg.get_option(ecg.ECG_OPT_ROW_SPLIT)
+        ecg.set_option(ecg.ECG_OPT_ROW_SPLIT, 0)
+        try:
+            ecg.matrix_apply_batch_multi(fused, blocks, out)
+        finally:
+            ecg.set_option(ecg.ECG_OPT_ROW_SPLIT, saved)
+
+    # "fused" is what a multi-row caller reaches: the engine splits the separable 40 -> 5 program into five
+    # 8 -> 1 row programs by itself (ECG_OPT_ROW_SPLIT); "fused_unsplit" is the same call without the split
     variants = {
         "rows": lambda: ecg.matrix_apply_batch_multi(rows, blocks, out, prog_of_stripe=prog_of, stripe_of=stripe_of),
         "fused": lambda: ecg.matrix_apply_batch_multi(fused, blocks, out),
+        "fused_unsplit": unsplit,
     }
     alg = S * 45 * B
     res = {}

@@ -1974,6 +1974,69 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
     return lease.done();
 }
 
+// Row split of a batched launch (ECG_OPT_ROW_SPLIT, include/ecg.h): when every program's output rows read
+// disjoint input sets of one size, each (stripe, row) runs as its own launch stripe over that row's inputs
+// only.  A PC merge's 40 -> 5 XOR then streams 8 blocks per workgroup instead of 40 (the fused form ran
+// at 0.72 of HBM peak against 0.76 for rows, profiles/r03/final/workloads/bench_pc-merge.log).  Rows
+// then run in different workgroups, so no output block may be an input block of the same stripe: the
+// split is taken only when the outputs provably overlap no input (disjoint spans, or, for equal stripe
+// strides, no output within B bytes of an input of its stripe).  Returns R = rows per program (0 = no
+// split) and the split programs, program p * R + r = row r of program p.
+static int row_split(const std::vector<LinearOp>& progs, int S, const void* in_base, long long iss, long long ibs,
+                     const void* out_base, long long oss, long long obs, long long B, bool has_stripe_of,
+                     std::vector<LinearOp>& rows) {
+    const long long min_k = get_option(ECG_OPT_ROW_SPLIT);
+    const int k = progs[0].k_in(), m = progs[0].m_out();
+    if (min_k <= 0 || k < min_k || m < 2 || k % m || (long long)S * m > 0x7fffffffLL) return 0;
+    const int kr = k / m;
+    int max_src = 0, max_dst = 0;
+    for (const LinearOp& op : progs) {
+        if (op.k_in() != k || op.m_out() != m || op.coef.size() != (size_t)k * m) return 0;
+        for (int j = 0; j < k; j++) {
+            int users = 0;
+            for (int r = 0; r < m; r++) users += op.coef[(size_t)r * k + j] != 0;
+            if (users != 1) return 0;
+        }
+        for (int r = 0; r < m; r++) {
+            int n = 0;
+            for (int j = 0; j < k; j++) n += op.coef[(size_t)r * k + j] != 0;
+            if (n != kr) return 0;
+        }
+        for (int id : op.src_ids) max_src = std::max(max_src, id);
+        for (int id : op.dst_ids) max_dst = std::max(max_dst, id);
+    }
+    const uintptr_t ib = (uintptr_t)in_base, ob = (uintptr_t)out_base;
+    bool safe = false;
+    if (!has_stripe_of) {
+        const uintptr_t i1 = ib + (uintptr_t)((S - 1) * iss + max_src * ibs + B);
+        const uintptr_t o1 = ob + (uintptr_t)((S - 1) * oss + max_dst * obs + B);
+        safe = i1 <= ob || o1 <= ib;
+    }
+    if (!safe && iss == oss) {
+        safe = true;
+        for (const LinearOp& op : progs)
+            for (int d : op.dst_ids)
+                for (int j : op.src_ids) {
+                    const long long delta = (long long)(ob + (uintptr_t)(d * obs)) - (long long)(ib + (uintptr_t)(j * ibs));
+                    if (delta > -B && delta < B) safe = false;
+                }
+    }
+    if (!safe) return 0;
+    rows.clear();
+    for (const LinearOp& op : progs)
+        for (int r = 0; r < m; r++) {
+            LinearOp one;
+            one.dst_ids.push_back(op.dst_ids[r]);
+            for (int j = 0; j < k; j++)
+                if (const uint8_t c = op.coef[(size_t)r * k + j]) {
+                    one.src_ids.push_back(op.src_ids[j]);
+                    one.coef.push_back(c);
+                }
+            rows.push_back(std::move(one));
+        }
+    return m;
+}
+
 int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of_stripe, int S,
                         const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
                         long long out_sstride, long long out_bstride, long long B, hipStream_t st,
@@ -1986,8 +2049,11 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
         if (rc != ECG_OK) return rc;
     }
     if (progs.size() > 1 && !d_prog_of_stripe) return ECG_EINVAL;
+    thread_local std::vector<LinearOp> rows;
+    const int R = row_split(progs, S, in_base, in_sstride, in_bstride, out_base, out_sstride, out_bstride, B,
+                            d_stripe_of != nullptr, rows);
     int status = ECG_OK;
-    std::shared_ptr<ProgramSet> ps = program_set(progs, &status, st);
+    std::shared_ptr<ProgramSet> ps = R ? program_set(rows, &status, st) : program_set(progs, &status, st);
     if (!ps) return status;
     if (const int rc = ps->ensure_ready(st); rc != ECG_OK) return rc;
     GfLaunch a;
@@ -2006,7 +2072,8 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
     a.B = B;
     a.k = ps->k;
     a.m = ps->m;
-    a.S = S;
+    a.S = R ? S * R : S;
+    a.row_split = R;
     a.MT = ps->MT;
     a.rtiles = ps->rtiles;
     a.binary = ps->binary ? 1 : 0;

@@ -197,6 +197,23 @@ __device__ __forceinline__ void wg_coords(const GfLaunch& a, int& s, int& w) {
     w = (int)(b - (long long)s * a.wg_per_stripe);
 }
 
+// The program of launch stripe s; s becomes the stripe it addresses.  Row split (STRIDED, row_split = R):
+// launch stripe s is output row s % R of stripe s / R, run as its own program (the host split each
+// program into R single-row programs whose inputs are that row's own, engine.cpp run_strided).
+template <int MODE>
+__device__ __forceinline__ int launch_prog(const GfLaunch& a, int& s) {
+    int r = 0;
+    if constexpr (MODE == GF_MODE_STRIDED) {
+        if (a.row_split) {
+            r = s % a.row_split;
+            s = s / a.row_split;
+        }
+    }
+    const int p = a.prog_of_stripe ? cst(a.prog_of_stripe)[s] : 0;
+    if constexpr (MODE == GF_MODE_STRIDED) return a.row_split ? p * a.row_split + r : p;
+    return p;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Generic vector path: bytes [0, 16 * floor(B / 16)) of every block; all pointers 16-byte aligned.
 // grid.x = S * wg_per_stripe (stripe-major), grid.y = row tiles of MT outputs.
@@ -205,7 +222,7 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
     int s, w;
     wg_coords(a, s, w);
     const int rt = blockIdx.y;
-    const int prog = a.prog_of_stripe ? cst(a.prog_of_stripe)[s] : 0;
+    const int prog = launch_prog<MODE>(a, s);
     const int k = a.k;
     const int row0 = rt * MT;
     const int nrows = min(MT, a.m - row0);
@@ -494,7 +511,7 @@ __global__ void __launch_bounds__(kThreads) gf_byte_kernel(const GfLaunch a) {
     int s, w;
     wg_coords(a, s, w);
     const int rt = blockIdx.y;
-    const int prog = a.prog_of_stripe ? cst(a.prog_of_stripe)[s] : 0;
+    const int prog = launch_prog<MODE>(a, s);
     const int k = a.k;
     const int row0 = rt * MT;
     const int nrows = min(MT, a.m - row0);
@@ -563,6 +580,7 @@ void init_options() {
     g_opt[ECG_OPT_MAP_GROUP].store(env("ECG_MAP_GROUP", 1));
     g_opt[ECG_OPT_LAT_DWORD_BYTES].store(env("ECG_LAT_DWORD_BYTES", 1 << 20));
     g_opt[ECG_OPT_CALL_WORKER].store(env("ECG_CALL_WORKER", 0));
+    g_opt[ECG_OPT_ROW_SPLIT].store(env("ECG_ROW_SPLIT", 16));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -701,6 +719,7 @@ int set_option(int opt, long long value) {
     if (opt == ECG_OPT_MAP_GROUP && (value < 1 || value > (1 << 20))) return -1;
     if (opt == ECG_OPT_LAT_DWORD_BYTES && value < 0) return -1;
     if (opt == ECG_OPT_CALL_WORKER && (value < 0 || value > 1000000)) return -1;  // idle limit <= 1 s
+    if (opt == ECG_OPT_ROW_SPLIT && value < 0) return -1;
     g_opt[opt].store(value);
     return 0;
 }

@@ -52,6 +52,8 @@ struct GfLaunch {
     const int* dst_ids;
     const int* prog_of_stripe;   // [S] or nullptr (program 0 for every stripe)
     const int* stripe_of;        // [S] or nullptr: launch stripe i addresses stripe stripe_of[i] (STRIDED)
+    int row_split;               // STRIDED: 0, or R -> launch stripe i is row i % R of stripe i / R (program
+                                 // prog_of_stripe[i / R] * R + i % R); S counts launch stripes
     // GF_MODE_STRIDED
     const uint8_t* in_base;
     uint8_t* out_base;

@@ -103,7 +103,12 @@ long long ecg_host_pinned_xfer_threshold(void);
                                  1 KiB: ~5 us instead of ~11 us per call.  The worker runs on a
                                  high-priority stream: leave it off in a process that runs its own work on
                                  high-priority streams */
-#define ECG_OPT_COUNT 8
+#define ECG_OPT_ROW_SPLIT 8 /* batched launches whose op's output rows read disjoint input sets of one size,
+                               with at least this many inputs in all (default 16; 0 = never), run each
+                               (stripe, row) as its own launch stripe reading only that row's inputs: a
+                               PC merge's 40 -> 5 XOR as five 8 -> 1 programs (fewer concurrent block
+                               streams per workgroup; profiles/r04/pc_merge/) */
+#define ECG_OPT_COUNT 9
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

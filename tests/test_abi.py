@@ -217,6 +217,9 @@ def test_tuning_options_validation(ecg):
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_CALL_WORKER, 2_000_000) != 0  # idle limit above 1 s
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_CALL_WORKER, 500) == 0
         assert ecg.get_option(ecg.ECG_OPT_CALL_WORKER) == 500
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_ROW_SPLIT, -1) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_ROW_SPLIT, 0) == 0  # never split
+        assert ecg.get_option(ecg.ECG_OPT_ROW_SPLIT) == 0
     finally:
         for o, v in enumerate(saved):
             ecg.set_option(o, v)
@@ -228,6 +231,8 @@ def test_tuning_options_validation(ecg):
         assert saved[ecg.ECG_OPT_LAT_DWORD_BYTES] == 1 << 20
     if "ECG_CALL_WORKER" not in os.environ:
         assert saved[ecg.ECG_OPT_CALL_WORKER] == 0  # off by default
+    if "ECG_ROW_SPLIT" not in os.environ:
+        assert saved[ecg.ECG_OPT_ROW_SPLIT] == 16
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])

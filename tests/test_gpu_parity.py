@@ -890,6 +890,83 @@ def test_matrix_apply_multi_with_stripe_subset(ecg, oracle, torch_cuda):
         assert np.array_equal(hout[s, 1], ref[0]) and np.array_equal(hout[s, 0], ref[1]), s
 
 
+def _apply_ref(oracle, progs, which, hin, S, B, out_rows):
+    """Host reference of matrix_apply_batch_multi: program which[s] of stripe s, all reads before writes."""
+    ref = np.zeros((S, out_rows, B), np.uint8)
+    for s in range(S):
+        coef, src, dst = progs[which[s]]
+        outs = [np.zeros(B, np.uint8) for _ in dst]
+        oracle.jerasure_matrix_encode(len(src), len(dst), [c for r in coef for c in r], [hin[s, j] for j in src],
+                                      outs, B)
+        for p, d in enumerate(dst):
+            ref[s, d] = outs[p]
+    return ref
+
+
+@pytest.mark.parametrize("split", [16, 0])
+def test_row_split_of_separable_programs(ecg, oracle, torch_cuda, split):
+    """ECG_OPT_ROW_SPLIT (engine.cpp row_split): programs whose output rows read disjoint input sets of one
+    size run one launch stripe per (stripe, row).  Same bytes as the unsplit launch, for a BINARY 40 -> 5 PC
+    merge shape, a GENERAL 16 -> 2 with two programs per launch over a stripe subset, tails and unaligned
+    block sizes; and an in-place op whose outputs are inputs of other rows is never split (its rows must all
+    read before any writes)."""
+    torch = torch_cuda
+    saved = ecg.get_option(ecg.ECG_OPT_ROW_SPLIT)
+    rng = random.Random(5)
+    try:
+        ecg.set_option(ecg.ECG_OPT_ROW_SPLIT, split)
+        # BINARY 40 -> 5, outputs in their own buffer
+        S, n, B = 9, 50, 65536 + 48
+        d_in = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(d_in, 31)
+        src = rng.sample(range(n), 40)
+        coef = [[1 if j // 8 == r else 0 for j in range(40)] for r in range(5)]
+        progs = [(coef, src, [4, 0, 3, 1, 2])]
+        out = torch.zeros((S, 5, B), dtype=torch.uint8, device="cuda")
+        ecg.matrix_apply_batch_multi(progs, d_in, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), _apply_ref(oracle, progs, [0] * S, d_in.cpu().numpy(), S, B, 5))
+        # GENERAL 16 -> 2, two programs (different row supports), stripe subset, B not a multiple of 16
+        S, n, B = 20, 24, 4096 + 5
+        d_in = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(d_in, 32)
+        progs = []
+        for _ in range(2):
+            src = rng.sample(range(n), 16)
+            cf = [[rng.randrange(1, 256) if (j < 8) == (r == 0) else 0 for j in range(16)] for r in range(2)]
+            progs.append((cf, src, [1, 0]))
+        subset = sorted(rng.sample(range(S), 13))
+        which = [rng.randrange(2) for _ in subset]
+        out = torch.zeros((S, 2, B), dtype=torch.uint8, device="cuda")
+        ecg.matrix_apply_batch_multi(progs, d_in, out, prog_of_stripe=torch.tensor(which, dtype=torch.int32,
+                                                                                    device="cuda"),
+                                     stripe_of=torch.tensor(subset, dtype=torch.int32, device="cuda"))
+        torch.cuda.synchronize()
+        hin, hout = d_in.cpu().numpy(), out.cpu().numpy()
+        wfull = [0] * S
+        for s, w in zip(subset, which):
+            wfull[s] = w
+        ref = _apply_ref(oracle, progs, wfull, hin, S, B, 2)
+        for s in range(S):
+            assert np.array_equal(hout[s], ref[s]) if s in subset else not hout[s].any(), s
+        # in place: row 0 writes block 16 (an input of row 1), row 1 writes block 0 (an input of row 0)
+        S, B = 6, 65536
+        d = torch.empty((S, 32, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(d, 33)
+        h0 = d.cpu().numpy()
+        cf = [[1 if (j < 16) == (r == 0) else 0 for j in range(32)] for r in range(2)]
+        progs = [(cf, list(range(32)), [16, 0])]
+        ecg.matrix_apply_batch_multi(progs, d, d)
+        torch.cuda.synchronize()
+        ref = h0.copy()
+        for s in range(S):
+            ref[s, 16] = np.bitwise_xor.reduce(h0[s, 0:16], axis=0)
+            ref[s, 0] = np.bitwise_xor.reduce(h0[s, 16:32], axis=0)
+        assert np.array_equal(d.cpu().numpy(), ref)
+    finally:
+        ecg.set_option(ecg.ECG_OPT_ROW_SPLIT, saved)
+
+
 @pytest.mark.parametrize("B,S", [(65536 + 48, 11), ((1 << 20) + 16, 9), (65536, 13), (1 << 20, 7)])
 @pytest.mark.parametrize("pinned", [False, True])
 def test_host_pipeline_encode_decode(ecg, oracle, torch_cuda, pinned, B, S):

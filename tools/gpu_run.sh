@@ -28,9 +28,9 @@ mkdir -p "$O"
 PYT="python -u -m pytest -p no:cacheprovider --timeout 120 --timeout-method thread"
 HEADLINE="--no-config5 --no-ring --no-host-path"
 
-run() {  # name limit cmd...
-  local name=$1 lim=$2; shift 2
-  timeout -k 10 "$lim" "$@"
+run() {  # name limit log cmd...  (the command's output goes to log; the status line to this script's stdout)
+  local name=$1 lim=$2 log=$3; shift 3
+  timeout -k 10 "$lim" "$@" >> "$log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   [ $rc -eq 0 ] || exit $rc
@@ -58,14 +58,15 @@ RINGS="lrc-repair-ring lrc-global-ring pc-merge-ring"
 
 for step in "$@"; do
   case $step in
-    tests) run tests 1200 $PYT tests -q -m gpu > "$O/pytest_gpu.log" 2>&1 || true
-           grep -E "^(FAILED|ERROR)|passed|failed" "$O/pytest_gpu.log" | tail -8 ;;
-    test:*) k=${step#test:}
-           run "test $k" 600 $PYT tests -v -s -m gpu -k "$k" > "$O/pytest_${k// /_}.log" 2>&1 || true
-           tail -3 "$O/pytest_${k// /_}.log" ;;
-    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1; tail -1 "$O/smoke.log" ;;
-    bench) run bench 500 python bench.py > "$O/bench.log" 2>&1; tail -1 "$O/bench.log" | cut -c1-400 ;;
-    headline) run headline 400 python bench.py --no-cpu-baseline $HEADLINE > "$O/bench_headline.log" 2>&1
+    tests) timeout -k 10 1200 $PYT tests -q -m gpu > "$O/pytest_gpu.log" 2>&1; rc=$?
+           grep -E "^(FAILED|ERROR)|passed|failed" "$O/pytest_gpu.log" | tail -8; echo "tests rc=$rc"
+           [ $rc -eq 0 ] || exit $rc ;;
+    test:*) k=${step#test:}; L="$O/pytest_${k// /_}.log"
+           timeout -k 10 600 $PYT tests -v -s -m gpu -k "$k" > "$L" 2>&1; rc=$?
+           tail -3 "$L"; echo "test $k rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    smoke) run smoke 300 "$O/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$O/smoke.log" ;;
+    bench) run bench 500 "$O/bench.log" python bench.py; tail -1 "$O/bench.log" | cut -c1-400 ;;
+    headline) run headline 400 "$O/bench_headline.log" python bench.py --no-cpu-baseline $HEADLINE
            tail -1 "$O/bench_headline.log" | cut -c1-400 ;;
     prof) prof prof prof.log --steps 40 --warmup 3 --no-cpu-baseline
           prof prof_headline prof_headline.log --steps 40 --warmup 3 --no-cpu-baseline $HEADLINE ;;
@@ -74,27 +75,27 @@ for step in "$@"; do
            "$O/pmc_traffic.json" rs104_B1048576_S4096 > /dev/null && echo "pmc parse ok" || exit 1 ;;
     summary) python tools/profile_summary.py "$O/prof_headline/run_kernel_trace.csv" "$O/pmc_traffic.json" \
                "$O/headline_profile.json" 40 > /dev/null && echo "summary ok" || exit 1 ;;
-    rehearsal) run rehearsal 600 bash tools/gpu_dist_rehearsal.sh > "$O/rehearsal.log" 2>&1; tail -3 "$O/rehearsal.log" ;;
-    rehearsal8) N=8 run rehearsal8 900 bash tools/gpu_dist_rehearsal.sh > "$O/rehearsal8.log" 2>&1; tail -3 "$O/rehearsal8.log" ;;
+    rehearsal) run rehearsal 600 "$O/rehearsal.log" bash tools/gpu_dist_rehearsal.sh; tail -3 "$O/rehearsal.log" ;;
+    rehearsal8) run rehearsal8 900 "$O/rehearsal8.log" env N=8 bash tools/gpu_dist_rehearsal.sh; tail -3 "$O/rehearsal8.log" ;;
     workloads) for w in $WORKLOADS; do
-                 run "bench $w" 500 python bench.py --workload $w --no-cpu-baseline > "$O/bench_$w.log" 2>&1
+                 run "bench $w" 500 "$O/bench_$w.log" python bench.py --workload $w --no-cpu-baseline
                done
                for w in $RINGS; do
-                 run "bench $w" 300 python bench.py --workload $w --self-p2p > "$O/bench_$w.log" 2>&1
+                 run "bench $w" 300 "$O/bench_$w.log" python bench.py --workload $w --self-p2p
                done ;;
     wprof) for w in rs-decode-patterns lrc-repair pc-merge rs4m-waves; do
              prof "wprof/$w" "wprof_$w.log" --workload $w --no-cpu-baseline
            done ;;
-    w:*) w=${step#w:}; run "bench $w" 500 python bench.py --workload $w --no-cpu-baseline > "$O/bench_$w.log" 2>&1
+    w:*) w=${step#w:}; run "bench $w" 500 "$O/bench_$w.log" python bench.py --workload $w --no-cpu-baseline
          tail -1 "$O/bench_$w.log" | cut -c1-600 ;;
     wp:*) w=${step#wp:}; prof "wprof/$w" "wprof_$w.log" --workload $w --no-cpu-baseline ;;
-    callrate) run call_rate 300 ./tools/call_rate > "$O/call_rate.txt" 2>&1
-              run record_cost 300 ./tools/record_cost > "$O/record_cost.txt" 2>&1 ;;
+    callrate) run call_rate 300 "$O/call_rate.txt" ./tools/call_rate
+              run record_cost 300 "$O/record_cost.txt" ./tools/record_cost ;;
     ab) for r in 1 2 3; do
           for v in new prev; do
             if [ $v = prev ]; then LP=$R/erasure-codes-prototype_amd/lib/ab; else LP=$R/erasure-codes-prototype_amd/lib; fi
-            LD_LIBRARY_PATH=$LP run "call_rate $v $r" 200 ./tools/call_rate 3 device > "$O/ab_${v}_$r.txt" 2>&1
-            LD_LIBRARY_PATH=$LP run "record_cost $v $r" 200 ./tools/record_cost >> "$O/ab_${v}_$r.txt" 2>&1
+            run "call_rate $v $r" 200 "$O/ab_${v}_$r.txt" env LD_LIBRARY_PATH=$LP ./tools/call_rate 3 device
+            run "record_cost $v $r" 200 "$O/ab_${v}_$r.txt" env LD_LIBRARY_PATH=$LP ./tools/record_cost
           done
         done
         grep -H -E "dev_matrix|record " "$O"/ab_*.txt | cut -c1-160 ;;
