@@ -12,7 +12,7 @@
 #   summary    tools/profile_summary.py over prof_headline's trace + pmc_traffic.json -> headline_profile.json
 #              (copy it and pmc_traffic.json to profiles/ to have bench.py's roofline name them)
 #   rehearsal  bench.py --gpus 2 on the one GPU (tools/gpu_dist_rehearsal.sh)
-#   rehearsal8 bench.py --gpus 8 on the one GPU, scaled down (tools/gpu_dist_rehearsal.sh, N=8)
+#   rehearsal8 bench.py --gpus 8 on the one GPU, scaled down (tools/gpu_dist_rehearsal8.sh + check_rehearsal_n.py)
 #   workloads  every bench.py --workload line                                    -> bench_<w>.log
 #   wprof      rocprofv3 kernel stats of each non-default workload
 #   w:<name>   one workload line                                                  -> bench_<name>.log
@@ -76,7 +76,7 @@ for step in "$@"; do
     summary) python tools/profile_summary.py "$O/prof_headline/run_kernel_trace.csv" "$O/pmc_traffic.json" \
                "$O/headline_profile.json" 40 > /dev/null && echo "summary ok" || exit 1 ;;
     rehearsal) run rehearsal 600 "$O/rehearsal.log" bash tools/gpu_dist_rehearsal.sh; tail -3 "$O/rehearsal.log" ;;
-    rehearsal8) run rehearsal8 900 "$O/rehearsal8.log" env N=8 bash tools/gpu_dist_rehearsal.sh; tail -3 "$O/rehearsal8.log" ;;
+    rehearsal8) run rehearsal8 1200 "$O/rehearsal8.log" env OUT=${OUT:-run}/rehearsal8 bash tools/gpu_dist_rehearsal8.sh; tail -3 "$O/rehearsal8.log" ;;
     workloads) for w in $WORKLOADS; do
                  run "bench $w" 500 "$O/bench_$w.log" python bench.py --workload $w --no-cpu-baseline
                done
