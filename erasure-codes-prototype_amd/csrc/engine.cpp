@@ -249,12 +249,16 @@ bool never_destroyed(hipStream_t st) { return st == nullptr || st == hipStreamPe
 //      one record per stream per pass;
 //   2. sets whose covers (and upload) have all fired are freed;
 //   3. the cover mask is rebuilt from the streams still waiting;
-//   4. unheld sets that cannot be covered (streams not seen again, overflow) beyond kGraveyardMax: the
-//      device is synchronized and every unheld set freed.
+//   4. unheld sets that cannot be covered (streams not seen again, overflow) beyond ECG_OPT_GRAVEYARD: the
+//      caller synchronizes the device outside the lock and frees them (sync_and_free_unheld).
 void Engine::sweep_retired(hipStream_t current, bool has_current) {
-    std::vector<std::shared_ptr<ProgramSet>> dead;  // destroyed after the lock is released
-    std::lock_guard<std::mutex> lk(rmu_);
-    sweep_locked(current, has_current, dead);
+    bool over = false;
+    {
+        std::vector<std::shared_ptr<ProgramSet>> dead;  // destroyed after the lock is released
+        std::lock_guard<std::mutex> lk(rmu_);
+        over = sweep_locked(current, has_current, dead);
+    }
+    if (over) (void)sync_and_free_unheld();  // the graveyard outgrew ECG_OPT_GRAVEYARD
 }
 
 // A launch on st hit the cover mask: cover the unheld retired sets that wait for st (one event record).
@@ -295,11 +299,11 @@ void Engine::cover_retired(hipStream_t st) {
     }
 }
 
-void Engine::sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead) {
+bool Engine::sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead) {
     if (retired_.empty()) {
         waiting_.clear();
         cover_mask_.store(0, std::memory_order_relaxed);
-        return;
+        return false;
     }
     std::shared_ptr<ProgramSet::CoverEvent> made[3];  // current, null stream, per-thread stream
     auto cover_for = [&](hipStream_t st) -> std::shared_ptr<ProgramSet::CoverEvent> {
@@ -347,59 +351,53 @@ void Engine::sweep_locked(hipStream_t current, bool has_current, std::vector<std
         if (unheld) graveyard++;
         i++;
     }
-    if (graveyard > kGraveyardMax) {
-        // on THIS engine's device, whatever the calling thread's current device is
-        int caller_dev = -1;
-        (void)hipGetDevice(&caller_dev);
-        const bool switched = caller_dev != device_ && hipSetDevice(device_) == hipSuccess;
-        const bool synced = hipDeviceSynchronize() == hipSuccess;
-        if (switched) (void)hipSetDevice(caller_dev);
-        if (synced) {
-            waiting_.clear();
-            for (size_t i = 0; i < retired_.size();) {
-                if (retired_[i].use_count() == 1) {
-                    dead.push_back(std::move(retired_[i]));
-                    retired_[i] = std::move(retired_.back());
-                    retired_.pop_back();
-                    continue;
-                }
-                i++;
-            }
-        }
-    }
     uint64_t mask = 0;
     for (auto& kv : waiting_) mask |= stream_bit(kv.first);
     cover_mask_.store(mask, std::memory_order_relaxed);
+    return graveyard > (size_t)get_option(ECG_OPT_GRAVEYARD);
 }
 
-size_t Engine::retired_pending() {
-    std::vector<std::shared_ptr<ProgramSet>> dead;
-    std::lock_guard<std::mutex> lk(rmu_);
-    sweep_locked(nullptr, false, dead);
-    return retired_.size();
-}
-
-size_t Engine::reclaim() {
-    std::vector<std::shared_ptr<ProgramSet>> dead;
-    std::lock_guard<std::mutex> lk(rmu_);
+// Synchronize the engine's device WITHOUT holding the retirement lock (launches that hit the cover mask
+// take it), then free the sets that nobody held before the synchronize began: their launches were all
+// enqueued by then.  Sets are named by serial number, not address (a freed set's address may be reused).
+size_t Engine::sync_and_free_unheld() {
+    std::vector<uint64_t> before;
+    {
+        std::lock_guard<std::mutex> lk(rmu_);
+        for (auto& ps : retired_)
+            if (ps.use_count() == 1) before.push_back(ps->serial);
+    }
     int caller_dev = -1;
     (void)hipGetDevice(&caller_dev);
     const bool switched = caller_dev != device_ && hipSetDevice(device_) == hipSuccess;
     const bool synced = hipDeviceSynchronize() == hipSuccess;
     if (switched) (void)hipSetDevice(caller_dev);
-    if (!synced) return retired_.size();
-    for (size_t i = 0; i < retired_.size();) {
-        if (retired_[i].use_count() == 1) {
-            dead.push_back(std::move(retired_[i]));
-            retired_[i] = std::move(retired_.back());
-            retired_.pop_back();
-        } else {
+    std::vector<std::shared_ptr<ProgramSet>> dead;
+    std::lock_guard<std::mutex> lk(rmu_);
+    if (synced) {
+        std::sort(before.begin(), before.end());
+        for (size_t i = 0; i < retired_.size();) {
+            if (std::binary_search(before.begin(), before.end(), retired_[i]->serial)) {
+                dead.push_back(std::move(retired_[i]));
+                retired_[i] = std::move(retired_.back());
+                retired_.pop_back();
+                continue;
+            }
             i++;
         }
     }
-    sweep_locked(nullptr, false, dead);  // rebuilds the cover mask
+    (void)sweep_locked(nullptr, false, dead);  // rebuilds the waiting index and the cover mask
     return retired_.size();
 }
+
+size_t Engine::retired_pending() {
+    std::vector<std::shared_ptr<ProgramSet>> dead;
+    std::lock_guard<std::mutex> lk(rmu_);
+    (void)sweep_locked(nullptr, false, dead);
+    return retired_.size();
+}
+
+size_t Engine::reclaim() { return sync_and_free_unheld(); }
 
 Engine::Engine(int device) : device_(device) {}
 
@@ -468,6 +466,8 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
         }
     }
     auto ps = std::make_shared<ProgramSet>();
+    static std::atomic<uint64_t> serials{0};
+    ps->serial = ++serials;
     ps->nprog = np;
     ps->k = k;
     ps->m = m;

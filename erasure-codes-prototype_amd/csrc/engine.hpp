@@ -40,6 +40,7 @@ class Engine;
 
 struct ProgramSet {
     Engine* owner = nullptr;  // its device memory (one block: tables + ids) goes back to owner's pool
+    uint64_t serial = 0;      // unique per set (retirement names sets by it, not by address)
     void* mem = nullptr;
     size_t mem_class = 0;
     CoefTab* d_tabs = nullptr;
@@ -58,7 +59,7 @@ struct ProgramSet {
     // stream is alive then, and a record then follows every earlier launch on it).  The null stream and
     // hipStreamPerThread are never destroyed, so they are covered at once.  A set whose streams are never
     // seen again (destroyed, or idle) waits in a bounded graveyard, emptied by a device synchronize when it
-    // outgrows kGraveyardMax or on ecg_program_sets_reclaim.  Host-tier launches are not noted: those calls
+    // outgrows ECG_OPT_GRAVEYARD or on ecg_program_sets_reclaim.  Host-tier launches are not noted: those calls
     // wait for their own completion before they return.  More than kMaxStreams streams -> graveyard.
     static constexpr int kMaxStreams = 8;
     struct CoverEvent;
@@ -165,12 +166,13 @@ private:
     // further launch can be enqueued), then until the cover event of every stream they were launched on has
     // fired (ProgramSet: covers are recorded on a stream only while the library holds it from a caller).
     // Swept on every cache miss, with the miss's stream as `current`; no device-wide synchronize unless the
-    // graveyard of sets that cannot be covered outgrows kGraveyardMax.
-    static constexpr size_t kGraveyardMax = 16384;
+    // graveyard of sets that cannot be covered outgrows ECG_OPT_GRAVEYARD.
     void retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted);
     void sweep_retired(hipStream_t current, bool has_current);
     void cover_retired(hipStream_t st);  // a launch on st hit the cover mask
-    void sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead);
+    // under rmu_: true = the graveyard outgrew ECG_OPT_GRAVEYARD (the caller then runs sync_and_free_unheld)
+    bool sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead);
+    size_t sync_and_free_unheld();
     static uint64_t stream_bit(hipStream_t st) {
         return 1ull << ((((uintptr_t)st >> 4) * 0x9E3779B97F4A7C15ull) >> 58);
     }

@@ -581,6 +581,7 @@ void init_options() {
     g_opt[ECG_OPT_LAT_DWORD_BYTES].store(env("ECG_LAT_DWORD_BYTES", 1 << 20));
     g_opt[ECG_OPT_CALL_WORKER].store(env("ECG_CALL_WORKER", 0));
     g_opt[ECG_OPT_ROW_SPLIT].store(env("ECG_ROW_SPLIT", 16));
+    g_opt[ECG_OPT_GRAVEYARD].store(env("ECG_GRAVEYARD", 16384));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -720,6 +721,7 @@ int set_option(int opt, long long value) {
     if (opt == ECG_OPT_LAT_DWORD_BYTES && value < 0) return -1;
     if (opt == ECG_OPT_CALL_WORKER && (value < 0 || value > 1000000)) return -1;  // idle limit <= 1 s
     if (opt == ECG_OPT_ROW_SPLIT && value < 0) return -1;
+    if (opt == ECG_OPT_GRAVEYARD && value < 1) return -1;
     g_opt[opt].store(value);
     return 0;
 }

@@ -48,8 +48,8 @@ int ecg_program_cache_size(void);  /* programs cached for the current device (di
  * its launches have completed, proven by an event the library records on each stream the set ran on the
  * next time a caller hands it that stream (the library never names a caller stream after the call that
  * passed it returns: callers may destroy their streams at any time).  Sets whose streams are not seen again
- * wait in a bounded graveyard, emptied by one device synchronize when it grows past 16384 sets, or by
- * ecg_program_sets_reclaim. */
+ * wait in a bounded graveyard, emptied by one device synchronize when it grows past ECG_OPT_GRAVEYARD sets
+ * (default 16384), or by ecg_program_sets_reclaim. */
 int ecg_program_sets_retiring(void);
 /* Synchronize the current device and free every evicted program set no call still holds (e.g. at idle, or
  * after a burst of per-request streams).  Returns the sets still retiring after it. */
@@ -108,7 +108,10 @@ long long ecg_host_pinned_xfer_threshold(void);
                                (stripe, row) as its own launch stripe reading only that row's inputs: a
                                PC merge's 40 -> 5 XOR as five 8 -> 1 programs (fewer concurrent block
                                streams per workgroup; profiles/r04/pc_merge/) */
-#define ECG_OPT_COUNT 9
+#define ECG_OPT_GRAVEYARD 9 /* evicted program sets allowed to wait for a stream the library is not handed
+                               again (a destroyed or idle caller stream) before one device synchronize
+                               frees them all (default 16384; >= 1; see ecg_program_sets_retiring) */
+#define ECG_OPT_COUNT 10
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

@@ -220,6 +220,8 @@ def test_tuning_options_validation(ecg):
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_ROW_SPLIT, -1) != 0
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_ROW_SPLIT, 0) == 0  # never split
         assert ecg.get_option(ecg.ECG_OPT_ROW_SPLIT) == 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_GRAVEYARD, 0) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_GRAVEYARD, 3) == 0
     finally:
         for o, v in enumerate(saved):
             ecg.set_option(o, v)
@@ -233,6 +235,8 @@ def test_tuning_options_validation(ecg):
         assert saved[ecg.ECG_OPT_CALL_WORKER] == 0  # off by default
     if "ECG_ROW_SPLIT" not in os.environ:
         assert saved[ecg.ECG_OPT_ROW_SPLIT] == 16
+    if "ECG_GRAVEYARD" not in os.environ:
+        assert saved[ecg.ECG_OPT_GRAVEYARD] == 16384
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])

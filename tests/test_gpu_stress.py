@@ -234,6 +234,7 @@ def _hip():
     h = ctypes.CDLL("libamdhip64.so.7")
     h.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
     h.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
     return h
 
 
@@ -311,3 +312,54 @@ def test_eviction_retires_across_destroyed_and_reused_streams(ecg, oracle):
         assert ecg.lib().ecg_program_sets_reclaim() == 0
     finally:
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
+
+
+def test_graveyard_bound_frees_sets_of_streams_never_seen_again(ecg, oracle):
+    """Evicted sets whose streams the library is never handed again cannot be covered (engine.hpp
+    ProgramSet): they wait in the graveyard, which one device synchronize empties once it outgrows
+    ECG_OPT_GRAVEYARD.  Forty per-request streams (all alive at once, so no handle is reused), each running
+    two distinct programs once and never used again; with a cache of 2 and a graveyard of 3, the retiring
+    count stays bounded and every result matches the oracle."""
+    import ctypes
+
+    import torch
+    hip = _hip()
+    saved = (ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE), ecg.get_option(ecg.ECG_OPT_GRAVEYARD))
+    rng = np.random.default_rng(23)
+    Bs = 4096
+    blocks = torch.from_numpy(rng.integers(0, 256, (4, Bs), dtype=np.uint8)).cuda()
+    host = blocks.cpu().numpy()
+    torch.cuda.synchronize()
+    try:
+        assert ecg.lib().ecg_program_sets_reclaim() == 0
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 2)
+        ecg.set_option(ecg.ECG_OPT_GRAVEYARD, 3)
+        peak = 0
+        streams = []
+        for _ in range(40):
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            streams.append(s)
+        assert len({x.value for x in streams}) == 40
+        for req, s in enumerate(streams):
+            outs = []
+            for j in range(2):
+                Mi = [int(x) for x in rng.integers(1, 256, 8)]
+                out = torch.zeros((2, Bs), dtype=torch.uint8, device="cuda")
+                assert ecg.dev_matrix_encode(4, 2, Mi, [blocks[i] for i in range(4)], [out[0], out[1]], Bs,
+                                             stream=s.value) == 0
+                outs.append((Mi, out))
+            hip.hipStreamSynchronize(s)
+            for Mi, out in outs:
+                want = [np.zeros(Bs, np.uint8) for _ in range(2)]
+                oracle.jerasure_matrix_encode(4, 2, Mi, [host[i] for i in range(4)], want, Bs)
+                assert np.array_equal(out.cpu().numpy(), np.stack(want)), req
+            peak = max(peak, ecg.lib().ecg_program_sets_retiring())
+        for s in streams:
+            assert hip.hipStreamDestroy(s) == 0
+        print(f"retiring peak {peak} with a graveyard of 3")
+        assert peak <= 3 + 4, peak  # the bound, plus the sets evicted by the last miss and not yet swept
+        assert ecg.lib().ecg_program_sets_reclaim() == 0
+    finally:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved[0])
+        ecg.set_option(ecg.ECG_OPT_GRAVEYARD, saved[1])
