@@ -35,7 +35,10 @@ Other workloads (--workload; measured for DESIGN.md, not the driver's BENCH line
   rs4m-waves  configs[4]: RS(10,4), 4 MiB blocks, 65536 stripes split over the ranks, encoded in
               HBM-resident waves of 1024 stripes (input regenerated per wave outside the timing);
   rs-host     configs[1] with the blocks in pinned HOST memory: the rate including hipMemcpyAsync to and
-              from the GPU over PCIe (H2D -> kernel -> D2H pipeline), for DESIGN.md.
+              from the GPU over PCIe (H2D -> kernel -> D2H pipeline), for DESIGN.md;
+  rs-small-host  configs[0]'s shape: RS(6,4), 1 KiB blocks, one jerasure_matrix_encode per stripe on
+              host buffers, issued from C++ (loopback/replay.cpp) as synchronous calls and inside batch
+              scopes with host deferral (ecg_batch_defer_host), beside the CPU baseline's per-stripe calls.
 
 Multi-GPU: one process per GPU (torch.distributed.run), stripes sharded per rank (ecg_dist), no
 data-path collective: rank 0's coding plan broadcast before the run, barrier + synchronize around the
@@ -82,7 +85,7 @@ def parse():
     ap.add_argument("--workload", default="rs-encode-decode",
                     choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "lrc-repair-ring", "lrc-global-ring",
                              "pc-merge", "pc-merge-ring",
-                             "rs4m-waves", "rs-host"])
+                             "rs4m-waves", "rs-host", "rs-small-host"])
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
     ap.add_argument("--chunk", type=int, default=None, help="lrc-repair-ring: stripes per transfer")
@@ -730,6 +733,8 @@ def replay_lib():
         L.ecg_replay_partial_repair.restype = I
         L.ecg_replay_partial_repair_mt.argtypes = [P, P, I, I, I, P, LL, LL, I, I, P, P, P, I, P, I, P, I, P, P, P, LL]
         L.ecg_replay_partial_repair_mt.restype = I
+        L.ecg_replay_host_encode.argtypes = [I, I, P, P, P, I, I, I, I]
+        L.ecg_replay_host_encode.restype = I
         _REPLAY = L
     return _REPLAY
 
@@ -1048,6 +1053,67 @@ def rs4m_waves(a, r):
 
 # ------------------------------------------------------------------------------- host-resident
 
+def rs_small_host(a, r):
+    """BASELINE configs[0]'s shape on the GPU: RS(6,4), 1 KiB blocks, one jerasure_matrix_encode per
+    stripe on host buffers (the proxy's SET loop, proxy.cpp:312-349), issued from C++ through the C ABI
+    (loopback/replay.cpp ecg_replay_host_encode).  Forms: one synchronous call per stripe; the same calls
+    in batch scopes with host deferral (ecg_batch_defer_host) of 64 stripes (config 1's object count) and of
+    all stripes.  The CPU baseline runs the oracle's per-stripe Jerasure-algorithm encode (SIMD split
+    tables) on one host thread over the same bytes (the reference's per-call path); every GPU form's
+    parities are compared with its output."""
+    import ctypes
+
+    import numpy as np
+    k, m = 6, 4
+    B = a.block_size or 1024
+    S = a.stripes or 4096
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    rng = np.random.default_rng(0xEC0DE + r.rank)
+    data = rng.integers(0, 256, (S, k, B), dtype=np.uint8)
+    rp = replay_lib()
+    mat = (ctypes.c_int * len(M))(*M)
+
+    def gpu(mode, per_scope):
+        coding = np.zeros((S, m, B), dtype=np.uint8)
+        rc = rp.ecg_replay_host_encode(k, m, mat, data.ctypes.data, coding.ctypes.data, B, S, mode, per_scope)
+        if rc:
+            raise ecg.EcgError(rc, "ecg_replay_host_encode")
+        return coding
+
+    res, outs = {}, {}
+    for name, mode, per in (("per_call_sync", 0, 1), ("deferred_scope_64", 1, 64), ("deferred_scope_all", 1, S)):
+        gpu(mode, per)  # warm-up (programs, contexts, staging)
+        ts = []
+        for _ in range(max(1, a.steps)):
+            t0 = time.perf_counter()
+            outs[name] = gpu(mode, per)
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        res[name] = {"us_per_stripe": round(t / S * 1e6, 3), "stripes_per_s": round(S / t, 1),
+                     "data_GiBps": round(S * k * B / t / 2 ** 30, 3)}
+    same = all(np.array_equal(outs[x], outs["per_call_sync"]) for x in outs)
+    line = {"workload": f"RS({k},{m}) {B} B blocks, {S} stripes, one jerasure_matrix_encode per stripe on host "
+                        "buffers (BASELINE configs[0] shape), issued from C++", "n_gpus": r.world,
+            "results": res, "gpu_forms_identical": same, "dtype": "u8",
+            "data": "synthetic (numpy PCG64 bytes, host memory)"}
+    if not a.no_cpu_baseline:
+        from oracle import ref
+        ref.lib()
+        cpu_out = np.zeros((S, m, B), dtype=np.uint8)
+        ts = []
+        for _ in range(max(3, a.steps)):
+            t0 = time.perf_counter()
+            ref.encode_batch_mt(k, m, M, data, cpu_out, B, S, 1)
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        line["cpu_baseline"] = {"us_per_stripe": round(t / S * 1e6, 3), "stripes_per_s": round(S / t, 1),
+                                "cores": 1, "kind": "port",
+                                "sample": f"{S} stripes, one SIMD split-table jerasure_matrix_encode per stripe, "
+                                          "1 thread (the proxy's per-call path)"}
+        line["gpu_equals_cpu_baseline"] = bool(np.array_equal(outs["per_call_sync"], cpu_out))
+    return line
+
+
 def rs_host(a, r):
     """RS(10,4), 1 MiB, host-resident (pinned) batch: encode and single-erasure decode including the
     PCIe copies (ecg_encode_batch_host / ecg_decode_batch_host pipelines), chunk size swept."""
@@ -1188,7 +1254,7 @@ def main():
     fn = {"rs-encode-decode": rs_encode_decode, "rs-decode-patterns": rs_decode_patterns, "lrc-repair": lrc_repair,
           "lrc-repair-ring": lrc_repair_ring, "lrc-global-ring": lrc_global_ring, "pc-merge": pc_merge,
           "pc-merge-ring": pc_merge_ring,
-          "rs4m-waves": rs4m_waves, "rs-host": rs_host}[a.workload]
+          "rs4m-waves": rs4m_waves, "rs-host": rs_host, "rs-small-host": rs_small_host}[a.workload]
     line = fn(a, r)
     if r.rank == 0:
         print(json.dumps(line), flush=True)

@@ -75,7 +75,8 @@ long long ecg_host_pinned_xfer_threshold(void) {
 }
 
 int ecg_batch_begin(void) { return batch_begin(); }
-int ecg_batch_flush(void) { return batch_flush(); }
+int ecg_batch_flush(void) { return batch_flush_all(); }
+int ecg_batch_defer_host(int on) { return batch_defer_host(on); }
 int ecg_batch_end(void) { return batch_end(); }
 int ecg_batch_scratch(const void* ptr, size_t bytes) { return batch_scratch(ptr, bytes); }
 int ecg_batch_last_stats(long long* recorded, long long* composed, long long* launches, long long* materialised) {

@@ -633,6 +633,27 @@ struct DeferScope {
         for (auto& e : order_evs) e.first->release_event(e.second);
         order_evs.clear();
     }
+    // Deferred HOST-tier calls (ecg_batch_defer_host): a call's input blocks are copied into the pinned
+    // staging of a host context leased for the scope when the call is made (region A, one slot per block
+    // read before written); its outputs get slots in region W and reach the caller's buffers at the flush.
+    // The flush moves region A in ONE H2D copy, launches the calls grouped by plan, moves W back in ONE D2H
+    // copy and scatters it -- the synchronous per-call round trip (launch + completion + two copies) is paid
+    // once per flush instead of once per call.  At most one of the two queues (device-tier q, host-tier hq)
+    // holds calls at any time: recording into one flushes the other first.
+    bool host_defer = false;
+    struct HostCall {
+        Engine* eng;
+        std::shared_ptr<const std::vector<LinearOp>> ops;
+        std::vector<uint8_t*> host;  // the caller's block pointers
+        std::vector<int> slot;       // >= 0: region-A slot; <= -2: region-W slot -2 - slot; -1: unused
+        std::vector<int> wr;         // block ids the call writes
+    };
+    std::vector<HostCall> hq;
+    int h_up = 0, h_w = 0;
+    long long h_B = -1;
+    bool h_inplace = false;                  // a written block has a region-A slot (read, then written)
+    std::unordered_map<uintptr_t, int> h_out;  // pending output block addresses
+    std::unique_ptr<CtxLease> h_ctx;
     ~DeferScope() { release_order_evs(); }
 };
 
@@ -763,6 +784,17 @@ int batch_begin() {
     t_defer.last_st = nullptr;
     t_defer.last_dev = -1;
     t_defer.last_recorded = false;
+    t_defer.host_defer = false;
+    return ECG_OK;
+}
+
+int batch_defer_host(int on) {
+    if (!t_defer.active) return ECG_EINVAL;
+    if (!on && !t_defer.hq.empty()) {
+        const int rc = host_flush();
+        if (rc != ECG_OK) return rc;
+    }
+    t_defer.host_defer = on != 0;
     return ECG_OK;
 }
 
@@ -1390,16 +1422,289 @@ int batch_flush() {
     return rc;
 }
 
-int batch_flush_pending() { return t_defer.q.empty() ? ECG_OK : batch_flush(); }
+int batch_flush_pending() {
+    if (!t_defer.hq.empty()) return host_flush();  // at most one queue holds calls
+    return t_defer.q.empty() ? ECG_OK : batch_flush();
+}
+
+int batch_flush_all() {
+    const int rh = t_defer.hq.empty() ? ECG_OK : host_flush();
+    const int rd = batch_flush();
+    return rh != ECG_OK ? rh : rd;
+}
 
 int batch_end() {
     if (!t_defer.active) return ECG_EINVAL;
     t_defer.active = false;  // the flush below is the scope's end: unconsumed scratch is not written
-    const int rc = batch_flush();
+    const int rh = t_defer.hq.empty() ? ECG_OK : host_flush();
+    const int rd = batch_flush();
+    const int rc = rh != ECG_OK ? rh : rd;
+    t_defer.host_defer = false;
     t_defer.q.clear();
     t_defer.scratch.clear();
     t_defer.release_order_evs();  // a later wait on one refers to its record at the time of the wait
     return rc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Deferred host-tier calls (DeferScope::hq; ecg_batch_defer_host).
+
+namespace {
+
+constexpr size_t kHostDeferMaxBytes = 64 << 20;  // staging (regions A + W) of one host batch
+
+// Pinned staging of the scope's context with room for `bytes`, keeping its first `keep` bytes.
+int ensure_pinned(HostCtx& c, size_t bytes, size_t keep) {
+    if (c.pinned_cap >= bytes) return ECG_OK;
+    const size_t cap = std::max(bytes, std::max(c.pinned_cap * 2, (size_t)1 << 20));
+    uint8_t* p = nullptr;
+    uint8_t* pd = nullptr;
+    ECG_HIP(hipHostMalloc((void**)&p, cap, hipHostMallocMapped | hipHostMallocCoherent));
+    if (hipHostGetDevicePointer((void**)&pd, p, 0) != hipSuccess) {
+        (void)hipHostFree(p);
+        set_last_error("hipHostGetDevicePointer(host batch staging) failed");
+        return ECG_EHIP;
+    }
+    if (keep && c.pinned) memcpy(p, c.pinned, keep);
+    if (c.pinned) {
+        if (c.stream) (void)hipStreamSynchronize(c.stream);
+        (void)hipHostFree(c.pinned);
+    }
+    c.pinned = p;
+    c.pinned_dev = pd;
+    c.pinned_cap = cap;
+    return ECG_OK;
+}
+
+void host_queue_reset() {
+    DeferScope& d = t_defer;
+    d.hq.clear();
+    d.h_out.clear();
+    d.h_up = d.h_w = 0;
+    d.h_B = -1;
+    d.h_inplace = false;
+    d.h_ctx.reset();  // a context whose batch did not complete drains its streams before its next lessee
+}
+
+}  // namespace
+
+// Record one host-tier call of an open scope with host deferral on.  Returns ECG_OK (recorded), a negative
+// status, or 1: not deferrable (blocks above kStagedMaxBlock, or the call alone overflows the staging) --
+// the caller runs it synchronously after flushing.  A call whose blocks include a pending output of an
+// earlier recorded call, or with another block size or engine, flushes the batch first (blocks are
+// compared by address: blocks of one scope are identical or disjoint).
+int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B) {
+    DeferScope& d = t_defer;
+    if (B > (long long)kStagedMaxBlock) return 1;
+    thread_local std::vector<char> upload, written, used, produced;
+    upload.assign(nblocks, 0);
+    written.assign(nblocks, 0);
+    used.assign(nblocks, 0);
+    produced.assign(nblocks, 0);
+    for (const LinearOp& op : ops) {
+        for (int id : op.src_ids) {
+            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+            if (!produced[id]) upload[id] = 1;
+            used[id] = 1;
+        }
+        for (int id : op.dst_ids) {
+            if (id < 0 || id >= nblocks || !blocks[id]) return ECG_EINVAL;
+            produced[id] = written[id] = used[id] = 1;
+        }
+    }
+    int nup = 0, nw = 0;
+    for (int id = 0; id < nblocks; id++) {
+        nup += upload[id];
+        nw += used[id] && !upload[id];
+    }
+    const size_t pitch = ((size_t)B + 255) & ~(size_t)255;
+    if ((size_t)(nup + nw) * pitch > kHostDeferMaxBytes) return 1;
+    if (!d.q.empty())
+        if (const int rc = batch_flush(); rc != ECG_OK) return rc;  // at most one queue holds calls
+    bool flush = !d.hq.empty() && (d.h_B != B || d.hq.back().eng != eng ||
+                                   (size_t)(d.h_up + d.h_w + nup + nw) * pitch > kHostDeferMaxBytes);
+    for (int id = 0; id < nblocks && !flush && !d.h_out.empty(); id++)
+        flush = used[id] && d.h_out.count((uintptr_t)blocks[id]);
+    if (flush)
+        if (const int rc = host_flush(); rc != ECG_OK) return rc;
+    if (!d.h_ctx) {
+        d.h_ctx = std::make_unique<CtxLease>(eng->device());
+        HostCtx& c = **d.h_ctx;
+        if (!c.stream && hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) {
+            host_queue_reset();
+            set_last_error("hipStreamCreate(host batch) failed");
+            return ECG_EHIP;
+        }
+        d.h_B = B;
+    }
+    HostCtx& c = **d.h_ctx;
+    if (const int rc = ensure_pinned(c, (size_t)(d.h_up + nup) * pitch, (size_t)d.h_up * pitch); rc != ECG_OK) {
+        host_queue_reset();
+        return rc;
+    }
+    DeferScope::HostCall call;
+    call.eng = eng;
+    call.host.assign(blocks, blocks + nblocks);
+    call.slot.assign(nblocks, -1);
+    for (int id = 0; id < nblocks; id++) {
+        if (upload[id]) {
+            call.slot[id] = d.h_up;
+            memcpy(c.pinned + (size_t)d.h_up * pitch, blocks[id], (size_t)B);  // inputs read at call time
+            d.h_up++;
+        } else if (used[id]) {
+            call.slot[id] = -2 - d.h_w++;
+        }
+        if (written[id]) {
+            call.wr.push_back(id);
+            d.h_out[(uintptr_t)blocks[id]] = 1;
+            d.h_inplace |= upload[id] != 0;
+        }
+    }
+    if (!d.hq.empty() && same_ops(*d.hq.back().ops, ops)) call.ops = d.hq.back().ops;
+    else call.ops = std::make_shared<const std::vector<LinearOp>>(ops);
+    d.hq.push_back(std::move(call));
+    return ECG_OK;
+}
+
+// Run the recorded host-tier calls: one H2D of region A, the calls' launches grouped by plan (consecutive
+// calls with one plan: one strided or pointer-table launch per op), one D2H of region W (and of A when a
+// call wrote a block it had read), then the outputs copied into the caller's buffers.  The queue is
+// emptied whatever happens; on an error the outputs of this batch are undefined.
+int host_flush() {
+    DeferScope& d = t_defer;
+    if (d.hq.empty()) return ECG_OK;
+    // The batch is taken out of the scope first: the launches below go through entry points that flush
+    // pending calls (run_strided), which must find nothing to flush.
+    struct Batch {
+        std::vector<DeferScope::HostCall> hq;
+        std::unique_ptr<CtxLease> ctx;
+    } bt;
+    bt.hq.swap(d.hq);
+    bt.ctx = std::move(d.h_ctx);
+    const int h_up = d.h_up, h_w = d.h_w;
+    const bool h_inplace = d.h_inplace;
+    const long long B = d.h_B;
+    host_queue_reset();
+    HostCtx& c = **bt.ctx;
+    hipStream_t st = c.stream;
+    Engine* eng = bt.hq[0].eng;
+    const size_t pitch = ((size_t)B + 255) & ~(size_t)255;
+    const size_t a_bytes = (size_t)h_up * pitch, total = (size_t)(h_up + h_w) * pitch;
+    auto fail = [&](int rc) { return rc; };  // bt's lease drains the context's streams on the way out
+    int caller_dev = -1;
+    (void)hipGetDevice(&caller_dev);
+    const bool switched = caller_dev != eng->device() && hipSetDevice(eng->device()) == hipSuccess;
+    struct Restore {
+        bool on;
+        int dev;
+        ~Restore() {
+            if (on) (void)hipSetDevice(dev);
+        }
+    } restore{switched, caller_dev};
+    if (c.cap < total) {
+        if (hipStreamSynchronize(st) != hipSuccess) return fail(ECG_EHIP);
+        if (c.scratch) (void)hipFree(c.scratch);
+        c.scratch = nullptr;
+        c.cap = 0;
+        if (hipMalloc(&c.scratch, total) != hipSuccess) {
+            set_last_error("hipMalloc(host batch scratch) failed");
+            return fail(ECG_EHIP);
+        }
+        c.cap = total;
+    }
+    if (const int rc = ensure_pinned(c, total, a_bytes); rc != ECG_OK) return fail(rc);
+    if (a_bytes && hipMemcpyAsync(c.scratch, c.pinned, a_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+        set_last_error("hipMemcpyAsync(host batch H2D) failed");
+        return fail(ECG_EHIP);
+    }
+    const size_t n = bt.hq.size();
+    thread_local std::vector<uint8_t*> dptr;
+    thread_local std::vector<size_t> first;
+    first.resize(n + 1);
+    size_t tot = 0;
+    for (size_t i = 0; i < n; i++) {
+        first[i] = tot;
+        tot += bt.hq[i].slot.size();
+    }
+    first[n] = tot;
+    dptr.assign(tot, nullptr);
+    for (size_t i = 0; i < n; i++) {
+        const auto& sl = bt.hq[i].slot;
+        for (size_t id = 0; id < sl.size(); id++) {
+            const int v = sl[id];
+            if (v >= 0) dptr[first[i] + id] = c.scratch + (size_t)v * pitch;
+            else if (v <= -2) dptr[first[i] + id] = c.scratch + a_bytes + (size_t)(-2 - v) * pitch;
+        }
+    }
+    // Calls of one shape -- the same number of ops, and per op the same (k_in, m_out) -- form one group
+    // whatever their coefficients (per-stripe decodes of different erasure patterns): the calls of a host
+    // batch touch disjoint staging slots, so any grouping keeps each call's own op order.  Per op, a group
+    // with one plan goes out as a strided launch (or a pointer table); mixed plans as ONE pointer-table
+    // launch with a program per matrix (run_ptr_batch_multi).
+    auto shape_of = [&](size_t i) {
+        std::vector<int> sig;
+        for (const LinearOp& op : *bt.hq[i].ops) {
+            sig.push_back(op.k_in());
+            sig.push_back(op.m_out());
+        }
+        return sig;
+    };
+    std::map<std::vector<int>, std::vector<size_t>> groups;
+    for (size_t i = 0; i < n; i++) groups[shape_of(i)].push_back(i);
+    int rc = ECG_OK;
+    std::vector<const uint8_t* const*> calls;
+    std::vector<const LinearOp*> per_call;
+    for (auto& kv : groups) {
+        const std::vector<size_t>& G = kv.second;
+        if (G.size() == 1) {
+            rc = eng->launch_direct(*bt.hq[G[0]].ops, dptr.data() + first[G[0]], B, st);
+            if (rc != ECG_OK) break;
+            continue;
+        }
+        calls.clear();
+        for (size_t i : G) calls.push_back(dptr.data() + first[i]);
+        const size_t nops = bt.hq[G[0]].ops->size();
+        for (size_t o = 0; o < nops && rc == ECG_OK; o++) {
+            const LinearOp& op0 = (*bt.hq[G[0]].ops)[o];
+            bool one_plan = true;
+            for (size_t i : G) one_plan &= bt.hq[i].ops.get() == bt.hq[G[0]].ops.get();
+            if (op0.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
+                for (size_t i : G)
+                    if (rc == ECG_OK) rc = eng->launch_direct({(*bt.hq[i].ops)[o]}, dptr.data() + first[i], B, st);
+            } else if (one_plan) {
+                bool done = false;
+                rc = eng->run_calls_strided(op0, calls, B, st, &done);
+                if (rc == ECG_OK && !done) rc = eng->run_ptr_batch(op0, calls, B, st);
+            } else {
+                per_call.clear();
+                for (size_t i : G) per_call.push_back(&(*bt.hq[i].ops)[o]);
+                rc = eng->run_ptr_batch_multi(per_call, calls, B, st);
+            }
+        }
+        if (rc != ECG_OK) break;
+    }
+    if (rc != ECG_OK) return fail(rc);
+    if (h_w && hipMemcpyAsync(c.pinned + a_bytes, c.scratch + a_bytes, total - a_bytes, hipMemcpyDeviceToHost, st) !=
+                     hipSuccess) {
+        set_last_error("hipMemcpyAsync(host batch D2H) failed");
+        return fail(ECG_EHIP);
+    }
+    if (h_inplace && hipMemcpyAsync(c.pinned, c.scratch, a_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
+        set_last_error("hipMemcpyAsync(host batch D2H) failed");
+        return fail(ECG_EHIP);
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        set_last_error("hipStreamSynchronize(host batch) failed");
+        return fail(ECG_EHIP);
+    }
+    for (const DeferScope::HostCall& call : bt.hq)
+        for (int id : call.wr) {
+            const int v = call.slot[id];
+            const size_t off = v >= 0 ? (size_t)v * pitch : a_bytes + (size_t)(-2 - v) * pitch;
+            memcpy(call.host[id], c.pinned + off, (size_t)B);
+        }
+    bt.ctx->done();
+    return ECG_OK;
 }
 
 int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* const*>& calls, long long B,
@@ -1446,6 +1751,124 @@ int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* c
     return rc;
 }
 
+// S calls of one op shape (k_in, m_out), call s running *ops[s] over its blocks calls[s]: ONE pointer-table
+// launch with one program per distinct coefficient matrix (prog_of_stripe), instead of one launch per
+// plan.  Programs are kept with canonical ids (the pointer table carries each call's own blocks), so calls
+// that differ only in which blocks they name share a program.
+int Engine::run_ptr_batch_multi(const std::vector<const LinearOp*>& ops, const std::vector<const uint8_t* const*>& calls,
+                                long long B, hipStream_t st) {
+    const int S = (int)calls.size();
+    if (S == 0 || B == 0) return ECG_OK;
+    if (ops.size() != calls.size()) return ECG_EINVAL;
+    const int k = ops[0]->k_in(), m = ops[0]->m_out();
+    if (k < 1 || m < 1) return ECG_EINVAL;
+    thread_local std::vector<LinearOp> progs;
+    thread_local std::vector<int> pid;
+    progs.clear();
+    pid.assign((size_t)S, 0);
+    const LinearOp* last = nullptr;
+    int last_id = -1;
+    for (int c = 0; c < S; c++) {
+        const LinearOp& op = *ops[c];
+        if (op.k_in() != k || op.m_out() != m) return ECG_EINVAL;
+        if (&op == last) {
+            pid[c] = last_id;
+            continue;
+        }
+        int id = -1;
+        for (size_t p = 0; p < progs.size() && id < 0; p++)
+            if (progs[p].coef == op.coef) id = (int)p;
+        if (id < 0) {
+            LinearOp canon;
+            canon.coef = op.coef;
+            for (int j = 0; j < k; j++) canon.src_ids.push_back(j);
+            for (int q = 0; q < m; q++) canon.dst_ids.push_back(k + q);
+            progs.push_back(std::move(canon));
+            id = (int)progs.size() - 1;
+        }
+        pid[c] = last_id = id;
+        last = &op;
+    }
+    if (progs.size() == 1) {  // one matrix: the plain pointer-table launch (its ids are the calls' own)
+        thread_local std::vector<std::vector<const uint8_t*>> own;
+        thread_local std::vector<const uint8_t* const*> rows;
+        own.resize((size_t)S);
+        rows.resize((size_t)S);
+        for (int c = 0; c < S; c++) {
+            own[c].assign((size_t)(k + m), nullptr);
+            for (int j = 0; j < k; j++) own[c][j] = calls[c][ops[c]->src_ids[j]];
+            for (int q = 0; q < m; q++) own[c][k + q] = calls[c][ops[c]->dst_ids[q]];
+            rows[c] = own[c].data();
+        }
+        return run_ptr_batch(progs[0], rows, B, st);
+    }
+    int status = ECG_OK;
+    std::shared_ptr<ProgramSet> ps = program_set(progs, &status, st);
+    if (!ps) return status;
+    if (const int rc = ps->ensure_ready(st); rc != ECG_OK) return rc;
+    const size_t n = (size_t)S * (k + m);
+    const size_t ptr_bytes = n * sizeof(void*), bytes = ptr_bytes + (size_t)S * sizeof(int);
+    TableSlot& t = g_tables[device_][g_table_next[device_].fetch_add(1, std::memory_order_relaxed) % kTableSlots];
+    std::lock_guard<std::mutex> lk(t.mu);
+    if (t.pending) {
+        ECG_HIP(hipEventSynchronize(t.ev));
+        t.pending = false;
+    }
+    if (!t.ev) ECG_HIP(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming));
+    if (t.cap < bytes) {
+        if (t.host) (void)hipHostFree(t.host);
+        if (t.dev) (void)hipFree(t.dev);
+        t.host = t.dev = nullptr;
+        t.cap = 0;
+        const size_t cap = std::max(bytes, (size_t)64 << 10);
+        ECG_HIP(hipHostMalloc(&t.host, cap, hipHostMallocDefault));
+        ECG_HIP(hipMalloc(&t.dev, cap));
+        t.cap = cap;
+    }
+    const uint8_t** h = (const uint8_t**)t.host;
+    int* hp = (int*)((uint8_t*)t.host + ptr_bytes);
+    bool aligned = true;
+    for (int c = 0; c < S; c++) {
+        const LinearOp& op = *ops[c];
+        for (int j = 0; j < k; j++) {
+            const uint8_t* p = calls[c][op.src_ids[j]];
+            aligned &= aligned16(p);
+            h[(size_t)c * k + j] = p;
+        }
+        for (int q = 0; q < m; q++) {
+            const uint8_t* p = calls[c][op.dst_ids[q]];
+            aligned &= aligned16(p);
+            h[(size_t)S * k + (size_t)c * m + q] = p;
+        }
+        hp[c] = pid[c];
+    }
+    ECG_HIP(hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, st));
+    GfLaunch a;
+    memset(&a, 0, sizeof(a));
+    a.tabs = ps->d_tabs;
+    a.src_ids = ps->d_src;
+    a.dst_ids = ps->d_dst;
+    a.src_ptrs = (const uint8_t* const*)t.dev;
+    a.dst_ptrs = (uint8_t* const*)((const uint8_t**)t.dev + (size_t)S * k);
+    a.prog_of_stripe = (const int*)((uint8_t*)t.dev + ptr_bytes);
+    a.B = B;
+    a.k = ps->k;
+    a.m = ps->m;
+    a.S = S;
+    a.MT = ps->MT;
+    a.rtiles = ps->rtiles;
+    a.binary = ps->binary ? 1 : 0;
+    const hipError_t e = launch_gf(a, GF_MODE_PTRS, aligned, st);
+    if (e != hipSuccess) {
+        set_last_error(std::string("launch_gf(pointer table, multi): ") + hipGetErrorString(e));
+        return ECG_EHIP;
+    }
+    note_launch(*ps, st);
+    ECG_HIP(hipEventRecord(t.ev, st));
+    t.pending = true;
+    return ECG_OK;
+}
+
 int Engine::launch_direct(const std::vector<LinearOp>& ops, uint8_t* const* blocks, long long B, hipStream_t st) {
     for (const LinearOp& op : ops) {
         int rc = launch_one(op, blocks, B, st, /*host_tier=*/false);
@@ -1470,6 +1893,8 @@ int Engine::run_device(const std::vector<LinearOp>& ops, uint8_t* const* blocks,
     if (const int rc = check_ids(ops, blocks, nblocks); rc != ECG_OK) return rc;
     if (t_defer.active) {
         if (ops.empty() || B == 0) return ECG_OK;
+        if (!t_defer.hq.empty())
+            if (const int rc = host_flush(); rc != ECG_OK) return rc;
         std::shared_ptr<const std::vector<LinearOp>> shared;
         if (!t_defer.q.empty() && same_ops(*t_defer.q.back().ops, ops)) shared = t_defer.q.back().ops;
         else shared = std::make_shared<const std::vector<LinearOp>>(ops);
@@ -1485,6 +1910,8 @@ int Engine::run_device(const std::shared_ptr<const std::vector<LinearOp>>& ops, 
     if (const int rc = check_ids(*ops, blocks, nblocks); rc != ECG_OK) return rc;
     if (t_defer.active) {  // recorded with the caller's (interned) plan: no copy
         if (ops->empty() || B == 0) return ECG_OK;
+        if (!t_defer.hq.empty())
+            if (const int rc = host_flush(); rc != ECG_OK) return rc;
         t_defer.q.push_back(DeferredCall{this, st, B, ops, std::vector<uint8_t*>(blocks, blocks + nblocks)});
         return t_defer.q.size() >= flush_at() ? batch_flush() : ECG_OK;
     }
@@ -1784,10 +2211,11 @@ int call_worker_stats(long long* calls, long long* launches, long long* relaunch
 // per block (each pageable copy is a driver-staged round trip).  Large calls copy block by block.
 int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B) {
     if (B < 0) return ECG_EINVAL;
-    if (!t_defer.q.empty()) {
-        const int rc = batch_flush();  // keep call order with deferred device calls
-        if (rc != ECG_OK) return rc;
+    if (t_defer.active && t_defer.host_defer && !ops.empty() && B > 0) {
+        const int rc = record_host(this, ops, blocks, nblocks, B);
+        if (rc <= 0) return rc;  // recorded (or refused); 1 = not deferrable: run it now, below
     }
+    if (const int rc = batch_flush_pending(); rc != ECG_OK) return rc;  // keep call order with recorded calls
     if (ops.empty() || B == 0) return ECG_OK;
     CtxLease lease(device_);
     HostCtx& c = *lease;
@@ -2044,10 +2472,7 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
     if (S < 0 || B < 0) return ECG_EINVAL;
     if (S == 0 || B == 0) return ECG_OK;  // empty batch: nothing to read or write
     if (!in_base || !out_base) return ECG_EINVAL;
-    if (!t_defer.q.empty()) {
-        const int rc = batch_flush();
-        if (rc != ECG_OK) return rc;
-    }
+    if (const int rc = batch_flush_pending(); rc != ECG_OK) return rc;
     if (progs.size() > 1 && !d_prog_of_stripe) return ECG_EINVAL;
     thread_local std::vector<LinearOp> rows;
     const int R = row_split(progs, S, in_base, in_sstride, in_bstride, out_base, out_sstride, out_bstride, B,
@@ -2128,10 +2553,7 @@ int Engine::run_host_pipeline(const LinearOp& prog, const void* h_in, long long 
     if (S < 0 || B < 0 || prog.k_in() < 1 || prog.m_out() < 1) return ECG_EINVAL;
     if (S == 0 || B == 0) return ECG_OK;
     if (!h_in || !h_out) return ECG_EINVAL;
-    if (!t_defer.q.empty()) {
-        const int rc = batch_flush();
-        if (rc != ECG_OK) return rc;
-    }
+    if (const int rc = batch_flush_pending(); rc != ECG_OK) return rc;
     if (chunk < 1) chunk = 16;
     if (chunk > S) chunk = S;
     const int kin = prog.k_in(), mout = prog.m_out();

@@ -115,6 +115,10 @@ public:
     // One op over S calls' block pointers (host arrays): uploads the pointer tables, then run_ptrs.
     int run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* const*>& call_blocks, long long B,
                       hipStream_t stream);
+    // Calls of one op shape with per-call ops (different coefficient matrices): ONE pointer-table launch
+    // with a program per distinct matrix.
+    int run_ptr_batch_multi(const std::vector<const LinearOp*>& ops, const std::vector<const uint8_t* const*>& calls,
+                            long long B, hipStream_t stream);
     // The same, as ONE strided launch when the calls' blocks form base + call * sstride + id * bstride
     // (checked pointer by pointer); *done = false (nothing launched) otherwise.
     int run_calls_strided(const LinearOp& op, const std::vector<const uint8_t* const*>& calls, long long B,
@@ -228,6 +232,11 @@ int batch_begin();
 int batch_flush();
 int batch_end();
 bool batch_active();
+// Host-tier calls of the scope are recorded too (ecg_batch_defer_host): see DeferScope::hq in engine.cpp.
+int batch_defer_host(int on);
+int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B);
+int host_flush();
+int batch_flush_all();  // both queues (ecg_batch_flush)
 // Declare [p, p + bytes) scratch for the rest of the current scope (ECG_EINVAL outside a scope).
 int batch_scratch(const void* p, size_t bytes);
 // Flush this thread's recorded calls, if any (entry points that launch directly call it first, so a

@@ -69,7 +69,8 @@ EXPORTS = [
     "ecg_cauchy_original_coding_matrix", "ecg_cauchy_improve_coding_matrix", "ecg_cauchy_n_ones",
     "ecg_jerasure_invert_matrix", "ecg_jerasure_matrix_multiply", "ecg_galois_region_xor",
     "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode", "ecg_jerasure_matrix_dotprod",
-    "ecg_batch_begin", "ecg_batch_flush", "ecg_batch_end", "ecg_batch_scratch", "ecg_batch_last_stats",
+    "ecg_batch_begin", "ecg_batch_flush", "ecg_batch_end", "ecg_batch_defer_host", "ecg_batch_scratch",
+    "ecg_batch_last_stats",
     "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
     "ecg_encode_batch",
     "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_make_decode_matrix", "ecg_region_xor_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
@@ -160,6 +161,7 @@ def lib():
         "ecg_call_worker_stats": ([ctypes.POINTER(LL)] * 3 + [ctypes.POINTER(I)], I),
         "ecg_batch_begin": ([], I),
         "ecg_batch_flush": ([], I),
+        "ecg_batch_defer_host": ([I], I),
         "ecg_batch_end": ([], I),
         "ecg_batch_scratch": ([P, ctypes.c_size_t], I),
         "ecg_batch_last_stats": ([ctypes.POINTER(LL)] * 4, I),
@@ -354,10 +356,19 @@ class batch:
     """Deferred-batch scope (ecg_batch_begin / ecg_batch_end): per-stripe device-tier calls made by this
     thread inside the `with` block are recorded and launched on exit, one launch per plan and op where no
     data dependence orders the calls apart.  `scratch(t)` declares a device tensor (or (ptr, nbytes))
-    scratch: partial results written there and read later in the scope are composed away."""
+    scratch: partial results written there and read later in the scope are composed away.  host=True also
+    defers host-tier calls (ecg_batch_defer_host): their outputs are written when the scope flushes."""
+
+    def __init__(self, host=False):
+        self.host = host
 
     def __enter__(self):
         _check(lib().ecg_batch_begin(), "batch_begin")
+        if self.host:
+            rc = lib().ecg_batch_defer_host(1)
+            if rc:
+                lib().ecg_batch_end()
+                _check(rc, "batch_defer_host")
         return self
 
     def flush(self):

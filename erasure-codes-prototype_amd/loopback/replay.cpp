@@ -99,4 +99,32 @@ int ecg_replay_partial_repair_mt(ecg_ec** ecs, void** streams, int nthreads, int
     return 0;
 }
 
+// Config 1's per-stripe host calls (proxy.cpp:312-349: one jerasure_matrix_encode per stripe on the
+// proxy's host buffers): data [S][k][B], coding [S][m][B] in host memory.  mode 0: one synchronous call
+// per stripe; mode 1: the same calls inside batch scopes of `per_scope` stripes with host deferral on
+// (ecg_batch_defer_host), the outputs written at each scope's end.
+int ecg_replay_host_encode(int k, int m, const int* matrix, char* data, char* coding, int B, int S, int mode,
+                           int per_scope) {
+    if (k < 1 || m < 1 || B < 0 || S < 0 || mode < 0 || mode > 1 || (mode == 1 && per_scope < 1)) return ECG_EINVAL;
+    std::vector<char*> dp(k), cp(m);
+    auto one = [&](int s) {
+        for (int j = 0; j < k; j++) dp[j] = data + ((long long)s * k + j) * B;
+        for (int j = 0; j < m; j++) cp[j] = coding + ((long long)s * m + j) * B;
+        return ecg_jerasure_matrix_encode(k, m, 8, (int*)matrix, dp.data(), cp.data(), B);
+    };
+    int rc = 0;
+    if (mode == 0) {
+        for (int s = 0; s < S && !rc; s++) rc = one(s);
+        return rc;
+    }
+    for (int s0 = 0; s0 < S && !rc; s0 += per_scope) {
+        if ((rc = ecg_batch_begin())) return rc;
+        rc = ecg_batch_defer_host(1);
+        for (int s = s0; s < S && s < s0 + per_scope && !rc; s++) rc = one(s);
+        const int re = ecg_batch_end();
+        if (!rc) rc = re;
+    }
+    return rc;
+}
+
 }  // extern "C"

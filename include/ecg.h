@@ -192,6 +192,18 @@ int ecg_dev_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const
 int ecg_batch_begin(void);
 int ecg_batch_flush(void);
 int ecg_batch_end(void);
+/* Inside a scope (ECG_EINVAL outside one): on = 1 defers HOST-tier calls of this thread too -- the
+ * Jerasure-level calls and ErasureCode handles in ECG_MEM_HOST mode with blocks of at most 256 KiB.  Such a
+ * call copies its input blocks into pinned staging when it is made (the caller may reuse them at once) and
+ * writes its output blocks when the scope flushes: at ecg_batch_flush() / ecg_batch_end(), when a later
+ * call of the scope reads or writes one of its output blocks (or uses another block size), when a
+ * device-tier or batched call is made, and when the staging reaches 64 MiB.  Until then the caller must
+ * not read those outputs.  A flush moves all staged inputs in one H2D copy, launches the calls grouped by
+ * plan and moves the outputs back in one D2H copy: the per-call launch and completion round trip of a
+ * synchronous host call (~10 us at 1 KiB, config 1's RS(6,4)) is paid once per flush.  Calls with larger
+ * blocks run synchronously, as outside a scope.  on = 0 flushes the deferred host calls and stops
+ * deferring; the flag resets at ecg_batch_begin. */
+int ecg_batch_defer_host(int on);
 /* Declare the device range [ptr, ptr + bytes) SCRATCH in the calling thread's scope (ECG_EINVAL outside
  * one).  The declaration holds until the scope ends and applies to every recorded call not yet flushed,
  * whether recorded before or after it.  A recorded call that writes a block inside scratch memory does
