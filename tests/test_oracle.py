@@ -69,6 +69,83 @@ def test_rs10_4_matches_survey_restatement(oracle):
         [1, 103, 156, 151, 123, 187, 166, 175, 244, 83] + [1, 220, 166, 123, 82, 143, 245, 40, 167, 122]
 
 
+def _clmul_11d(a, b):
+    """GF(2^8)/0x11d product by shift-and-add (no tables): independent of the oracle's field code."""
+    r = 0
+    while b:
+        if b & 1:
+            r ^= a
+        b >>= 1
+        a <<= 1
+        if a & 0x100:
+            a ^= 0x11D
+    return r
+
+
+def _closed_form_vandermonde(k, m):
+    """The systematic Vandermonde coding matrix from its closed form, by a route that shares no step with
+    the oracle's column elimination (oracle/jerasure_w8.c:121-169):
+      * V = the (k+m) x k extended Vandermonde matrix: row 0 = e_0 (point 0), row k+m-1 = e_{k-1} (the point
+        at infinity), row i = (1, i, i^2, ...) in between (Plank & Ding, "Note: Correction to the 1997
+        tutorial on Reed-Solomon coding", 2005; Jerasure 2.0 reed_sol_extended_vandermonde_matrix);
+      * the systematic form is V * inv(V_top): the top k x k is invertible (distinct points) and every leading
+        minor of V_top is a Vandermonde minor, so the library's column elimination reaches it with no swap;
+      * then the library's two normalisations (reed_sol_big_vandermonde_distribution_matrix): each column
+        of the coding rows divided by its entry in coding row 0, then each coding row divided by its column-0
+        entry.
+    The inverse is Gauss-Jordan over GF(2^8) with row pivoting, written here from scratch."""
+    n = k + m
+    mul = _clmul_11d
+    inv_tab = [0] * 256
+    for a in range(1, 256):
+        inv_tab[a] = next(b for b in range(1, 256) if mul(a, b) == 1)
+
+    def row(i):
+        if i == 0:
+            return [1] + [0] * (k - 1)
+        if i == n - 1 and n > 1:
+            return [0] * (k - 1) + [1]
+        out, x = [], 1
+        for _ in range(k):
+            out.append(x)
+            x = mul(x, i)
+        return out
+
+    V = [row(i) for i in range(n)]
+    A = [r[:] + [int(i == j) for j in range(k)] for i, r in enumerate(V[:k])]
+    for c in range(k):
+        p = next(r for r in range(c, k) if A[r][c])
+        A[c], A[p] = A[p], A[c]
+        s = inv_tab[A[c][c]]
+        A[c] = [mul(s, x) for x in A[c]]
+        for r in range(k):
+            if r != c and A[r][c]:
+                f = A[r][c]
+                A[r] = [x ^ mul(f, y) for x, y in zip(A[r], A[c])]
+    inv_top = [r[k:] for r in A]
+    C = [[0] * k for _ in range(m)]
+    for i in range(m):
+        for j in range(k):
+            acc = 0
+            for t in range(k):
+                acc ^= mul(V[k + i][t], inv_top[t][j])
+            C[i][j] = acc
+    for j in range(k):
+        s = inv_tab[C[0][j]]
+        for i in range(m):
+            C[i][j] = mul(C[i][j], s)
+    for i in range(1, m):
+        s = inv_tab[C[i][0]]
+        C[i] = [mul(x, s) for x in C[i]]
+    return [x for r in C for x in r]
+
+
+@pytest.mark.parametrize("k,m", [(k, m) for k in range(1, 17) for m in range(1, 7)] +
+                         [(10, 4), (12, 4), (20, 4), (24, 8), (40, 16), (64, 8), (100, 4)])
+def test_vandermonde_matches_closed_form(oracle, k, m):
+    assert oracle.reed_sol_vandermonde_coding_matrix(k, m) == _closed_form_vandermonde(k, m)
+
+
 def test_cauchy(oracle):
     assert oracle.cauchy_n_ones(1) == 8
     assert oracle.cauchy_n_ones(2) == 11  # columns 2,4,..,128,29: seven single bits + popcount(0x1d)=4
