@@ -297,12 +297,47 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
 // one DWORD column per lane instead of 16 bytes.  A 1 KiB call is 64 sixteen-byte columns, i.e. ONE wave
 // that runs the whole multiply (~550 VALU instructions per lane for RS(6,4)) after its PCIe loads; at 4
 // bytes per lane the same bytes are 256 lanes in 4 waves on 4 SIMDs, each with a quarter of the multiply.
-// KB = the input count rounded up to a bucket (k <= KB): straight-line code over KB inputs, so the
-// compiler issues every input load AND every coefficient-table scalar load up front.  With a runtime
-// `if (u < k)` per input each table fetch sat behind its own branch: k dependent L2 round trips after
-// the PCIe loads (~1.7 us of a 6.6 us kernel, rocprofv3 kernel trace vs the plain-copy probe).  Padded
-// inputs (u >= k) re-read input 0 with table 0 and are masked out of the sum.
+// KB = the input count rounded up to a bucket (k <= KB): straight-line code over KB inputs, every input
+// load in flight at once.  Padded inputs (u >= k) re-read input 0 with table 0 and are masked out of the sum.
 // kLatThreads dword columns per workgroup; grid.x = ceil((B / 4) / kLatThreads), grid.y = row tiles.
+//
+// Coefficient tables through LDS (round 4).  The row tile's k * MT tables are k * MT * 5 dwords: 200 for
+// RS(10,4), more than the SGPR file holds, so as scalar loads they came in ~40 dependent rounds of
+// s_load + s_waitcnt lgkmcnt(0) (plus SGPR spills to VGPR lanes), each an L2 round trip when a CU's first
+// wave runs -- and a single call has about one wave per CU.  A 64 KiB RS(10,4) device call took 5.8 us of
+// kernel time for 896 KiB of traffic (profiles/r04/lat_tables/).  Now every wave fetches the tile's tables
+// with one to four 16-byte loads per lane, issued BEFORE its data loads (loads return in order, so waiting
+// for them does not wait for the data), writes them into its own LDS slice and reads them back, input by
+// input, as VGPR operands of v_perm (lat_fold_lds).  A wave reads only its own slice, in program order, so
+// no barrier is needed.
+template <int MT, int KB>
+struct LatTabs {
+    static constexpr int kPieces = KB * MT * 2;             // 16-byte pieces of the largest tile of this bucket
+    static constexpr int kPerLane = (kPieces + 63) / 64;    // loads per lane
+    CoefTab t[kLatThreads / 64][KB * MT];                   // one slice per wave
+};
+
+template <int MT, int KB>
+__device__ __forceinline__ void lat_tabs_load(const GfLaunch& a, int rt, u32x4 (&tv)[LatTabs<MT, KB>::kPerLane]) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.tabs + (size_t)rt * (size_t)a.k * MT);
+    const int last = a.k * MT * 2 - 1;  // this tile's last piece (k <= KB)
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < LatTabs<MT, KB>::kPerLane; ++i) tv[i] = src[min(lane + 64 * i, last)];
+}
+
+template <int MT, int KB>
+__device__ __forceinline__ const CoefTab* lat_tabs_store(LatTabs<MT, KB>& lds,
+                                                         const u32x4 (&tv)[LatTabs<MT, KB>::kPerLane]) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    u32x4* dst = reinterpret_cast<u32x4*>(lds.t[wave]);
+#pragma unroll
+    for (int i = 0; i < LatTabs<MT, KB>::kPerLane; ++i)
+        if (lane + 64 * i < LatTabs<MT, KB>::kPieces) dst[lane + 64 * i] = tv[i];
+    return lds.t[wave];
+}
+
+// The resident call worker's fold: tables in the constant address space (SGPRs).
 template <int MT, bool BIN, int KB>
 __device__ __forceinline__ void lat_fold(const int k, const ECG_CONST CoefTab* T, const uint32_t (&x)[KB],
                                          uint32_t (&acc)[MT]) {
@@ -323,51 +358,99 @@ __device__ __forceinline__ void lat_fold(const int k, const ECG_CONST CoefTab* T
     }
 }
 
-// EAGER (blocks <= kLatEagerBytes): lanes past the end load the last column and store nothing, so no
-// branch precedes the loads (block size, pointers and k come in fewer rounds of kernel-argument loads),
-// every pointer slot is loaded and then selected (no wait for k), and a scheduling barrier issues every
-// input load before the first coefficient-table load.  RS(6,4) 1 KiB host calls 0.3-2 us faster (A/B
-// of two builds over two boxes, profiles/r02/lat_kernel/eager/); single device calls at 64 KiB - 1 MiB
-// measured 1-5 % slower with it (the barrier raises register use), so only small blocks take it.
+// The latency kernel's fold over its LDS tables, read just in time: input u + 1's tables are read while
+// input u is folded, so at most two inputs' tables are live in VGPRs.  Hoisting all of them (what the
+// compiler does otherwise) costs k * MT * 5 VGPRs: 243 VGPRs for RS(10,4) -- two waves per SIMD -- and a
+// scratch spill for a 16-input, 8-output tile; read just in time they take 60 and 71.  The order is pinned
+// by an empty asm per input that consumes the accumulators and clobbers memory: input u's folds are done
+// before it, and input u + 2's LDS reads cannot move above it (a scheduling barrier does not hold: instruction
+// selection already sinks the arithmetic to its last use and hoists the loads).
+template <int MT, bool BIN, int KB>
+__device__ __forceinline__ void lat_fold_lds(const int k, const CoefTab* T, const uint32_t (&x)[KB],
+                                             uint32_t (&acc)[MT]) {
+    struct R {
+        uint32_t t0lo, t0hi, t1lo, t1hi, t2;
+    };
+    auto rd = [&](int u, R (&r)[MT]) {
+        const CoefTab* t = T + (size_t)(u < k ? u : 0) * MT;
+#pragma unroll
+        for (int p = 0; p < MT; ++p) {
+            if constexpr (BIN) r[p].t0lo = t[p].mask;
+            else r[p] = {t[p].t0lo, t[p].t0hi, t[p].t1lo, t[p].t1hi, t[p].t2};
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < MT; ++p) acc[p] = 0u;
+    R cur[MT], nxt[MT];
+    rd(0, cur);
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+        if (u + 1 < KB) rd(u + 1, nxt);
+        const uint32_t keep = u < k ? ~0u : 0u;  // uniform: padded inputs (u >= k) are masked out
+        if constexpr (BIN) {
+#pragma unroll
+            for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], x[u], cur[p].t0lo & keep, 0x78);
+        } else {
+            const Split sp = split(x[u]);
+#pragma unroll
+            for (int p = 0; p < MT; ++p) {
+                const uint32_t g = xor3(perm(cur[p].t0hi, cur[p].t0lo, sp.i0), perm(cur[p].t1hi, cur[p].t1lo, sp.i1),
+                                        perm(cur[p].t2, cur[p].t2, sp.i2));
+                acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], g, keep, 0x78);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < MT; ++p) asm volatile("" : "+v"(acc[p]) : : "memory");
+        if (u + 1 < KB)
+#pragma unroll
+            for (int p = 0; p < MT; ++p) cur[p] = nxt[p];
+    }
+}
+
+// EAGER (blocks <= kLatEagerBytes): a scheduling barrier keeps every input load ahead of the fold.  RS(6,4)
+// 1 KiB host calls 0.3-2 us faster (A/B of two builds over two boxes, profiles/r02/lat_kernel/eager/);
+// single device calls at 64 KiB - 1 MiB measured 1-5 % slower with it, so only small blocks take it.
+// Every lane runs the whole body: lanes past the end load the last column and store nothing, so no branch
+// precedes the loads and a wave past the end still reaches the flag epilogue.
 template <int MT, bool BIN, int KB, bool EAGER>
 __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLaunch a) {
+    __shared__ LatTabs<MT, KB> lds;
     const int rt = blockIdx.y;
     const int k = a.k;
     const int row0 = rt * MT;
     const int nrows = min(MT, a.m - row0);
-    const ECG_CONST CoefTab* T = cst(a.tabs) + (size_t)rt * (size_t)k * MT;
     const long long ndw = a.B >> 2;
     const long long c = (long long)blockIdx.x * kLatThreads + threadIdx.x;
-    if constexpr (EAGER) {
-        const bool live = c < ndw;
-        const long long off = (live ? c : ndw - 1) << 2;
-        uint32_t x[KB];
+    // Every input pointer slot is read with a constant index and then selected (a.isrc has kInlineSrc >= KB
+    // slots, the unused ones zeroed): one round of kernel-argument loads, no address computed from k.
+    const uint8_t* src[KB];
 #pragma unroll
-        for (int u = 0; u < KB; ++u) {
-            const uint8_t* pu = a.isrc[u];  // a.isrc has kInlineSrc >= KB slots, the unused ones zeroed
-            x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>((u < k ? pu : a.isrc[0]) + off));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        uint32_t acc[MT];
-        lat_fold<MT, BIN, KB>(a.k, T, x, acc);
-        if (live) {
+    for (int u = 0; u < KB; ++u) src[u] = a.isrc[u];
 #pragma unroll
-            for (int p = 0; p < MT; ++p)
-                if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(a.idst[row0 + p] + off));
-        }
-    } else if (c < ndw) {
-        const long long off = c << 2;
-        uint32_t x[KB];
+    for (int u = 1; u < KB; ++u) src[u] = u < k ? src[u] : src[0];
+    uint8_t* dst[MT];  // the output pointers and the flag word in the same round (not after the fold)
 #pragma unroll
-        for (int u = 0; u < KB; ++u)
-            x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(a.isrc[u < k ? u : 0] + off));
-        uint32_t acc[MT];
-        lat_fold<MT, BIN, KB>(a.k, T, x, acc);
+    for (int p = 0; p < MT; ++p) dst[p] = a.idst[min(row0 + p, kInlineDst - 1)];
+    unsigned* const flags = a.done_flags;
+    // the table loads go out first
+    u32x4 tv[LatTabs<MT, KB>::kPerLane];
+    lat_tabs_load<MT, KB>(a, rt, tv);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool live = c < ndw;
+    const long long off = (live ? c : ndw - 1) << 2;
+    uint32_t x[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u) x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(src[u] + off));
+    if constexpr (EAGER) __builtin_amdgcn_sched_barrier(0);
+    const CoefTab* T = lat_tabs_store<MT, KB>(lds, tv);
+    uint32_t acc[MT];
+    lat_fold_lds<MT, BIN, KB>(k, T, x, acc);
+    if (live) {
 #pragma unroll
         for (int p = 0; p < MT; ++p)
-            if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(a.idst[row0 + p] + off));
+            if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(dst[p] + off));
     }
-    if (a.done_flags) post_done_flag(a);
+    if (flags) post_done_flag(flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq);
 }
 
 // ---------------------------------------------------------------------------------------------

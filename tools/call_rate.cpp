@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (long long B : {64LL << 10, 256LL << 10, 1LL << 20}) {
+    for (long long B : {64LL << 10, 256LL << 10, 1LL << 20, 4LL << 20}) {
         if (host_latency_only) break;
         const int S = (int)std::min(4096LL, (16LL << 30) / (n * B));
         uint8_t* buf;

@@ -24,10 +24,10 @@ def main():
             grid = (row.get("Grid_Size_X") or row.get("Grid_Size", "?"), row.get("Grid_Size_Y", ""))
             dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
             groups.setdefault((name, grid), []).append(dur)
-    print(f"{'kernel':70s} {'grid':>14s} {'n':>3s} {'avg ms':>9s} {'min ms':>9s} {'med ms':>9s}")
+    print(f"{'kernel':70s} {'grid':>14s} {'n':>6s} {'avg us':>10s} {'min us':>10s} {'med us':>10s}")
     for (name, grid), d in sorted(groups.items()):
-        print(f"{name[:70]:70s} {'x'.join(g for g in grid if g):>14s} {len(d):3d} {statistics.mean(d) / 1e6:9.3f} "
-              f"{min(d) / 1e6:9.3f} {statistics.median(d) / 1e6:9.3f}")
+        print(f"{name[:70]:70s} {'x'.join(g for g in grid if g):>14s} {len(d):6d} {statistics.mean(d) / 1e3:10.2f} "
+              f"{min(d) / 1e3:10.2f} {statistics.median(d) / 1e3:10.2f}")
 
 
 if __name__ == "__main__":
