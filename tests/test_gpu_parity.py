@@ -97,6 +97,14 @@ def _latency_kernel_shapes(ecg, oracle):
             oracle.jerasure_matrix_encode(k, m, M, data, a, B)
             ecg.jerasure_matrix_encode(k, m, M, data, b, B)
             assert same(a, b), (B, k, m, kind)
+    for B, k, m in ((1024, 6, 32), (16384, 16, 20)):  # several row tiles, up to 32 outputs
+        M = [rng.randrange(256) for _ in range(k * m)]
+        data = [rnd(B, 9100 + j) for j in range(k)]
+        a = [rnd(B, 9200 + i) for i in range(m)]
+        b = [x.copy() for x in a]
+        oracle.jerasure_matrix_encode(k, m, M, data, a, B)
+        ecg.jerasure_matrix_encode(k, m, M, data, b, B)
+        assert same(a, b), (B, k, m)
 
 
 def test_flagged_calls_never_read_stale(ecg, oracle, torch_cuda):
@@ -617,6 +625,16 @@ def test_device_tier_single_call_latency_kernel(ecg, oracle, torch_cuda, lat_dwo
                 M = ([rng.randrange(2) for _ in range(k * m)] if k % 2 else
                      [rng.randrange(256) for _ in range(k * m)])
                 host = [rnd(B, 300 * k + j + B) for j in range(k)]
+                dev_data = [torch.from_numpy(h).cuda() for h in host]
+                dev_cod = [torch.zeros(B, dtype=torch.uint8, device="cuda") for _ in range(m)]
+                ecg.dev_matrix_encode(k, m, M, dev_data, dev_cod, B)
+                cases.append((B, k, m, M, host, dev_cod))
+        # many outputs: several row tiles per call, up to the 32 inline output pointers (each tile reads its
+        # own tables and output pointers)
+        for B, k, m in ((65536, 4, 17), (65536, 16, 32), (4096, 10, 24), (1 << 20, 12, 32)):
+            for binary in (False, True):
+                M = [rng.randrange(2) if binary else rng.randrange(256) for _ in range(k * m)]
+                host = [rnd(B, 77 * k + j + m) for j in range(k)]
                 dev_data = [torch.from_numpy(h).cuda() for h in host]
                 dev_cod = [torch.zeros(B, dtype=torch.uint8, device="cuda") for _ in range(m)]
                 ecg.dev_matrix_encode(k, m, M, dev_data, dev_cod, B)
