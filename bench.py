@@ -424,18 +424,52 @@ def rs_encode_decode(a, r):
     # the headline's buffers go before config 5 allocates its wave
     del arena, stripes, rebuilt, data, coding, pattern_of_stripe, idx, step, evs
     torch.cuda.empty_cache()
-    if not a.no_config5:
-        line["config5"] = config5(a, r, M, k, m)
-    if not a.no_host_path:
-        line["host_path"] = host_path_line(a, r, M, k, m)
-    if not a.no_ring:
-        sc = lambda n: max(8, int(n * a.ring_scale)) // 8 * 8  # noqa: E731
-        line["ring_repair"] = ring_repair_line(a, r, S=sc(1024))
-        line["global_ring_repair"] = ring_repair_line(a, r, S=sc(256), glob=True)
-        line["merge_ring"] = merge_ring_line(a, r, S=sc(64))
+    def optional():
+        if not a.no_config5:
+            line["config5"] = config5(a, r, M, k, m)
+        if not a.no_host_path:
+            line["host_path"] = host_path_line(a, r, M, k, m)
+        if not a.no_ring:
+            sc = lambda n: max(8, int(n * a.ring_scale)) // 8 * 8  # noqa: E731
+            line["ring_repair"] = ring_repair_line(a, r, S=sc(1024))
+            line["global_ring_repair"] = ring_repair_line(a, r, S=sc(256), glob=True)
+            line["merge_ring"] = merge_ring_line(a, r, S=sc(64))
+
+    optional_section(line, r, ["config5", "host_path", "ring_repair", "global_ring_repair", "merge_ring"], optional)
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line
+
+
+def optional_deadline_s() -> float:
+    """Seconds the line's optional sub-objects (config 5, host path, cross-GPU objects) may take before the
+    headline is printed without them (ECG_BENCH_OPTIONAL_DEADLINE_S).  Below the ranks' collective timeout
+    (ECG_DIST_TIMEOUT_S), whose watchdog would otherwise end every rank first -- with no line at all."""
+    env = os.environ.get("ECG_BENCH_OPTIONAL_DEADLINE_S")
+    return float(env) if env else 0.8 * D.timeout_s()
+
+
+def optional_section(line, r, keys, body):
+    """Run body(), which fills line[key] for `keys`, under ecg_dist.deadline: a sub-object that hangs (an
+    RCCL exchange across GPUs that never completes, say) must not cost the line the headline measured
+    before it.  On expiry rank 0 prints the line with {"error": ...} for every key not filled yet, and
+    every rank exits 0.  Exceptions inside the sub-objects are caught by the sub-objects themselves."""
+    limit = optional_deadline_s()
+
+    def expire():
+        try:
+            partial = dict(line)
+            for key in keys:
+                if key not in partial:
+                    partial[key] = {"error": f"not finished within {limit:.0f} s (optional-section deadline, "
+                                             "ECG_BENCH_OPTIONAL_DEADLINE_S); the rest of the line stands"}
+            if r.rank == 0:
+                print(json.dumps(partial), flush=True)
+        finally:
+            os._exit(0)
+
+    with D.deadline(limit, expire):
+        body()
 
 
 def config5(a, r, M, k, m):
@@ -1221,7 +1255,17 @@ def launch_check(a, r):
         ranks = [x.tolist() for x in out]
     else:
         ranks = [me]
-    return {"metric": METRIC, "n_gpus": r.world, "launch_check": True, "ranks": ranks}
+    line = {"metric": METRIC, "n_gpus": r.world, "launch_check": True, "ranks": ranks}
+    stall = os.environ.get("ECG_BENCH_TEST_STALL_OPTIONAL")  # fault injection for tests/test_dist_cpu.py only
+
+    def optional():
+        if stall is not None and int(stall) == r.rank:
+            time.sleep(3600)  # this rank never reaches the collective below
+        D.barrier(r)
+        line["optional"] = {"ok": True}
+
+    optional_section(line, r, ["optional"], optional)
+    return line
 
 
 def main():

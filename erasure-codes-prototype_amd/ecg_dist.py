@@ -16,8 +16,10 @@ the chunks around it.
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -58,6 +60,29 @@ DEFAULT_TIMEOUT_S = 300.0
 
 def timeout_s() -> float:
     return float(os.environ.get("ECG_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+
+
+@contextlib.contextmanager
+def deadline(seconds: float, on_expiry):
+    """Run the body; if it has not finished `seconds` after entry, call on_expiry() from a watchdog thread.
+    on_expiry must end the process (os._exit): the body may be stuck inside a collective that no Python
+    code can interrupt.  Finishing first (normally or by an exception) disarms it.  seconds <= 0: no
+    deadline.  Every rank arms its own, so a section that hangs on one rank ends on all of them."""
+    if seconds is None or seconds <= 0:
+        yield
+        return
+    done = threading.Event()
+
+    def watch():
+        if not done.wait(seconds):
+            on_expiry()
+
+    t = threading.Thread(target=watch, name="ecg-deadline", daemon=True)
+    t.start()
+    try:
+        yield
+    finally:
+        done.set()
 
 
 def init(r: Rank, backend: str = "nccl", device=None) -> None:

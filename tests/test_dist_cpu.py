@@ -274,6 +274,52 @@ def test_bench_stalled_rank_fails_within_dist_timeout():
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
 
 
+def test_bench_optional_section_deadline_keeps_the_line():
+    """A sub-object of the line that hangs on one rank (injected: ECG_BENCH_TEST_STALL_OPTIONAL, the other
+    rank waits for it in a collective) must not cost the line: every rank's optional-section deadline
+    (0.8 x ECG_DIST_TIMEOUT_S) fires before the collective timeout would abort the ranks, rank 0 prints the
+    line with an error object for the unfinished key, and every rank exits 0."""
+    import json
+    import subprocess
+    import time
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
+                        "--timeout", "200"], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=_bench_env(ECG_BENCH_TEST_STALL_OPTIONAL="1", ECG_DIST_TIMEOUT_S="20"))
+    took = time.time() - t0
+    assert p.returncode == 0, (p.returncode, p.stderr[-2000:])
+    assert took < 100, took
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    assert lines[0]["n_gpus"] == 2 and len(lines[0]["ranks"]) == 2
+    assert "deadline" in lines[0]["optional"]["error"]
+    # without the stall the same section completes
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
+                        "--timeout", "200"], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=_bench_env(ECG_DIST_TIMEOUT_S="20"))
+    assert p.returncode == 0, p.stderr[-2000:]
+    (line,) = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert line["optional"] == {"ok": True}
+
+
+def test_deadline_disarms_and_fires():
+    """ecg_dist.deadline: a body that finishes first disarms it; one that does not triggers on_expiry."""
+    sys.path[:0] = [os.path.join(ROOT, "erasure-codes-prototype_amd")]
+    import threading
+    import time
+    import ecg_dist as D
+    fired = threading.Event()
+    with D.deadline(0.5, fired.set):
+        pass
+    time.sleep(1.0)
+    assert not fired.is_set()
+    with D.deadline(0.2, fired.set):
+        time.sleep(1.0)
+    assert fired.is_set()
+    with D.deadline(0, lambda: (_ for _ in ()).throw(AssertionError("no deadline at 0"))):
+        time.sleep(0.1)
+
+
 def test_bench_launcher_watchdog_kills_stuck_ranks():
     """The launcher's wall-clock watchdog (--timeout): with the ranks' own timeout far away, a stuck rank
     is killed with its whole process group and bench.py exits 124 shortly after the limit."""
