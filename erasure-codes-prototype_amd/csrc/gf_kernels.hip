@@ -337,28 +337,7 @@ __device__ __forceinline__ const CoefTab* lat_tabs_store(LatTabs<MT, KB>& lds,
     return lds.t[wave];
 }
 
-// The resident call worker's fold: tables in the constant address space (SGPRs).
-template <int MT, bool BIN, int KB>
-__device__ __forceinline__ void lat_fold(const int k, const ECG_CONST CoefTab* T, const uint32_t (&x)[KB],
-                                         uint32_t (&acc)[MT]) {
-#pragma unroll
-    for (int p = 0; p < MT; ++p) acc[p] = 0u;
-#pragma unroll
-    for (int u = 0; u < KB; ++u) {
-        const ECG_CONST CoefTab* t = T + (size_t)(u < k ? u : 0) * MT;
-        const uint32_t keep = u < k ? ~0u : 0u;  // uniform
-        if constexpr (BIN) {
-#pragma unroll
-            for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], x[u], t[p].mask & keep, 0x78);
-        } else {
-            const Split sp = split(x[u]);
-#pragma unroll
-            for (int p = 0; p < MT; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], gmul(t[p], sp), keep, 0x78);
-        }
-    }
-}
-
-// The latency kernel's fold over its LDS tables, read just in time: input u + 1's tables are read while
+// The fold of the latency kernel and the call worker over LDS tables, read just in time: input u + 1's tables are read while
 // input u is folded, so at most two inputs' tables are live in VGPRs.  Hoisting all of them (what the
 // compiler does otherwise) costs k * MT * 5 VGPRs: 243 VGPRs for RS(10,4) -- two waves per SIMD -- and a
 // scratch spill for a 16-input, 8-output tile; read just in time they take 60 and 71.  The order is pinned
@@ -470,24 +449,48 @@ __device__ __forceinline__ unsigned long long wk_ptr(const unsigned* d, int q) {
     return ((unsigned long long)d[worker_pos(q + 1)] << 32) | d[worker_pos(q)];
 }
 
+// The call's tables go through the wave's LDS slice `wt` as in the latency kernel (one to two 16-byte loads
+// per lane, issued before the data loads; lat_fold_lds): through SGPRs they spilled 1324 SGPRs to VGPR
+// lanes in this kernel.  A generation is at least as wide as its calls (CallWorker: W >= need), so a lane
+// has at most one column; the loop after it is a backstop.
 template <int MT, bool BIN, int KB>
-__device__ __forceinline__ void worker_call(const unsigned* d) {
+__device__ __forceinline__ void worker_call(const unsigned* d, CoefTab* wt) {
     const int k = (int)d[worker_pos(WF_K)];
     const int m = (int)d[worker_pos(WF_M)];
     const long long ndw = (long long)d[worker_pos(WF_B)] >> 2;
-    const ECG_CONST CoefTab* T = (const ECG_CONST CoefTab*)(uintptr_t)wk_ptr(d, WF_TABS);
+    const u32x4* tg = reinterpret_cast<const u32x4*>((uintptr_t)wk_ptr(d, WF_TABS));
     const uint8_t* in[KB];
 #pragma unroll
     for (int u = 0; u < KB; u++) in[u] = (const uint8_t*)(uintptr_t)wk_ptr(d, WF_IN + 2 * (u < k ? u : 0));
     uint8_t* out[MT];
 #pragma unroll
     for (int p = 0; p < MT; p++) out[p] = (uint8_t*)(uintptr_t)wk_ptr(d, WF_OUT + 2 * (p < m ? p : 0));
-    for (long long c = (long long)blockIdx.x * kLatThreads + threadIdx.x; c < ndw; c += (long long)gridDim.x * kLatThreads) {
-        uint32_t x[KB];
+    constexpr int kPieces = KB * MT * 2, kPerLane = (kPieces + 63) / 64;
+    const int last = k * MT * 2 - 1, lane = threadIdx.x & 63;
+    u32x4 tv[kPerLane];
+#pragma unroll
+    for (int i = 0; i < kPerLane; ++i) tv[i] = tg[min(lane + 64 * i, last)];
+    __builtin_amdgcn_sched_barrier(0);
+    const long long stride = (long long)gridDim.x * kLatThreads;
+    long long c = (long long)blockIdx.x * kLatThreads + threadIdx.x;
+    const bool live = c < ndw;
+    uint32_t x[KB];
+#pragma unroll
+    for (int u = 0; u < KB; u++) x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(in[u]) + (live ? c : 0));
+#pragma unroll
+    for (int i = 0; i < kPerLane; ++i)
+        if (lane + 64 * i < kPieces) reinterpret_cast<u32x4*>(wt)[lane + 64 * i] = tv[i];
+    uint32_t acc[MT];
+    lat_fold_lds<MT, BIN, KB>(k, wt, x, acc);
+    if (live) {
+#pragma unroll
+        for (int p = 0; p < MT; p++)
+            if (p < m) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(out[p]) + c);
+    }
+    for (c += stride; c < ndw; c += stride) {
 #pragma unroll
         for (int u = 0; u < KB; u++) x[u] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(in[u]) + c);
-        uint32_t acc[MT];
-        lat_fold<MT, BIN, KB>(k, T, x, acc);
+        lat_fold_lds<MT, BIN, KB>(k, wt, x, acc);
 #pragma unroll
         for (int p = 0; p < MT; p++)
             if (p < m) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(out[p]) + c);
@@ -495,29 +498,30 @@ __device__ __forceinline__ void worker_call(const unsigned* d) {
 }
 
 template <int MT, bool BIN>
-__device__ __forceinline__ void worker_call_k(const unsigned* d) {
+__device__ __forceinline__ void worker_call_k(const unsigned* d, CoefTab* wt) {
     const unsigned k = d[worker_pos(WF_K)];
-    if (k <= 4) worker_call<MT, BIN, 4>(d);
-    else if (k <= 6) worker_call<MT, BIN, 6>(d);
-    else if (k <= 8) worker_call<MT, BIN, 8>(d);
-    else if (k <= 10) worker_call<MT, BIN, 10>(d);
-    else if (k <= 12) worker_call<MT, BIN, 12>(d);
-    else worker_call<MT, BIN, 16>(d);
+    if (k <= 4) worker_call<MT, BIN, 4>(d, wt);
+    else if (k <= 6) worker_call<MT, BIN, 6>(d, wt);
+    else if (k <= 8) worker_call<MT, BIN, 8>(d, wt);
+    else if (k <= 10) worker_call<MT, BIN, 10>(d, wt);
+    else if (k <= 12) worker_call<MT, BIN, 12>(d, wt);
+    else worker_call<MT, BIN, 16>(d, wt);
 }
 
 template <bool BIN>
-__device__ __forceinline__ void worker_call_m(const unsigned* d) {
+__device__ __forceinline__ void worker_call_m(const unsigned* d, CoefTab* wt) {
     switch (d[worker_pos(WF_M)]) {
-        case 1: worker_call_k<1, BIN>(d); break;
-        case 2: worker_call_k<2, BIN>(d); break;
-        case 3: worker_call_k<3, BIN>(d); break;
-        default: worker_call_k<4, BIN>(d); break;
+        case 1: worker_call_k<1, BIN>(d, wt); break;
+        case 2: worker_call_k<2, BIN>(d, wt); break;
+        case 3: worker_call_k<3, BIN>(d, wt); break;
+        default: worker_call_k<4, BIN>(d, wt); break;
     }
 }
 
 __global__ void __launch_bounds__(kLatThreads, 1) gf_call_worker_kernel(const WorkerArgs a) {
     __shared__ unsigned d[64];
     __shared__ unsigned go;  // set by thread 0 only: every exit decision is one for the whole workgroup
+    __shared__ CoefTab wtabs[kLatThreads / 64][kWorkerMaxSrc * kWorkerMaxRows];  // one table slice per wave
     const int tid = threadIdx.x;
     const bool leader = blockIdx.x == 0;
     unsigned next = a.start_seq;
@@ -573,8 +577,9 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_call_worker_kernel(const Wo
         // otherwise read lines of an earlier call's inputs still held in the CU / L2 caches (every call
         // after the first one read stale data without this, tests/test_gpu_worker.py).
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        if (d[worker_pos(WF_BINARY)]) worker_call_m<true>(d);
-        else worker_call_m<false>(d);
+        CoefTab* const wt = wtabs[tid >> 6];
+        if (d[worker_pos(WF_BINARY)]) worker_call_m<true>(d, wt);
+        else worker_call_m<false>(d, wt);
         post_done_flag(a.flags + (size_t)slot * kWorkerMaxWG + blockIdx.x, next);
         next++;
         last = wall_clock64();
