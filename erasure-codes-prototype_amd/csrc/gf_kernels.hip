@@ -337,13 +337,14 @@ __device__ __forceinline__ const CoefTab* lat_tabs_store(LatTabs<MT, KB>& lds,
     return lds.t[wave];
 }
 
-// The fold of the latency kernel and the call worker over LDS tables, read just in time: input u + 1's tables are read while
-// input u is folded, so at most two inputs' tables are live in VGPRs.  Hoisting all of them (what the
-// compiler does otherwise) costs k * MT * 5 VGPRs: 243 VGPRs for RS(10,4) -- two waves per SIMD -- and a
-// scratch spill for a 16-input, 8-output tile; read just in time they take 60 and 71.  The order is pinned
-// by an empty asm per input that consumes the accumulators and clobbers memory: input u's folds are done
-// before it, and input u + 2's LDS reads cannot move above it (a scheduling barrier does not hold: instruction
-// selection already sinks the arithmetic to its last use and hoists the loads).
+// The fold of the latency kernel and the call worker over LDS tables, read just in time: input u + 1's
+// tables are read while input u is folded, so at most two inputs' tables are live in VGPRs.  Hoisting all
+// of them (what the compiler does otherwise) costs k * MT * 5 VGPRs: 243 VGPRs for RS(10,4) -- two waves
+// per SIMD -- and a scratch spill for a 16-input, 8-output tile; read just in time they take 60 and 71
+// (tests/test_kernel_resources.py).  The order is pinned by an empty asm per input that consumes the
+// accumulators and clobbers memory: input u's folds are done before it, and input u + 2's LDS reads cannot
+// move above it (a scheduling barrier does not hold: instruction selection already sinks the arithmetic to
+// its last use and hoists the loads).
 template <int MT, bool BIN, int KB>
 __device__ __forceinline__ void lat_fold_lds(const int k, const CoefTab* T, const uint32_t (&x)[KB],
                                              uint32_t (&acc)[MT]) {
