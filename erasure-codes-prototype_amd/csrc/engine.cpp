@@ -1,6 +1,7 @@
 // GF(2^8) region engine.  See engine.hpp.
 #include "engine.hpp"
 
+#include <emmintrin.h>
 #include <string.h>
 
 #include <algorithm>
@@ -652,7 +653,8 @@ struct DeferScope {
     int h_up = 0, h_w = 0;
     long long h_B = -1;
     bool h_inplace = false;                  // a written block has a region-A slot (read, then written)
-    std::unordered_map<uintptr_t, int> h_out;  // pending output block addresses
+    PtrGroups h_out;                           // pending output block addresses (wr = 1), open addressing
+    size_t h_nout = 0;
     std::unique_ptr<CtxLease> h_ctx;
     ~DeferScope() { release_order_evs(); }
 };
@@ -1451,6 +1453,27 @@ int batch_end() {
 
 namespace {
 
+// Copy a call's input block into the scope's pinned staging with non-temporal stores.  Region A of a
+// host batch grows to tens of MiB (4096 RS(6,4) 4 KiB stripes: 96 MiB), far past the caches, and ordinary
+// stores pay a read-for-ownership of every destination line: the plain memcpy moved 7.8 GB/s and was most
+// of a recorded call's 3.2 us (tools/defer_cost.cpp, profiles/r04/small_host/).  The flush issues an
+// sfence before the H2D copy reads the region.  dst is 256-byte aligned (the slot pitch).
+void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    size_t i = 0;
+    if (((uintptr_t)dst & 15) == 0)
+        for (; i + 64 <= n; i += 64) {
+            const __m128i a = _mm_loadu_si128((const __m128i*)(src + i));
+            const __m128i b = _mm_loadu_si128((const __m128i*)(src + i + 16));
+            const __m128i c = _mm_loadu_si128((const __m128i*)(src + i + 32));
+            const __m128i d = _mm_loadu_si128((const __m128i*)(src + i + 48));
+            _mm_stream_si128((__m128i*)(dst + i), a);
+            _mm_stream_si128((__m128i*)(dst + i + 16), b);
+            _mm_stream_si128((__m128i*)(dst + i + 32), c);
+            _mm_stream_si128((__m128i*)(dst + i + 48), d);
+        }
+    if (i < n) memcpy(dst + i, src + i, n - i);
+}
+
 constexpr size_t kHostDeferMaxBytes = 64 << 20;  // staging (regions A + W) of one host batch
 
 // Pinned staging of the scope's context with room for `bytes`, keeping its first `keep` bytes.
@@ -1479,7 +1502,8 @@ int ensure_pinned(HostCtx& c, size_t bytes, size_t keep) {
 void host_queue_reset() {
     DeferScope& d = t_defer;
     d.hq.clear();
-    d.h_out.clear();
+    if (d.h_nout) d.h_out.reset(0);
+    d.h_nout = 0;
     d.h_up = d.h_w = 0;
     d.h_B = -1;
     d.h_inplace = false;
@@ -1523,8 +1547,8 @@ int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* b
         if (const int rc = batch_flush(); rc != ECG_OK) return rc;  // at most one queue holds calls
     bool flush = !d.hq.empty() && (d.h_B != B || d.hq.back().eng != eng ||
                                    (size_t)(d.h_up + d.h_w + nup + nw) * pitch > kHostDeferMaxBytes);
-    for (int id = 0; id < nblocks && !flush && !d.h_out.empty(); id++)
-        flush = used[id] && d.h_out.count((uintptr_t)blocks[id]);
+    for (int id = 0; id < nblocks && !flush && d.h_nout; id++)
+        flush = used[id] && d.h_out.last_write(blocks[id]) > 0;
     if (flush)
         if (const int rc = host_flush(); rc != ECG_OK) return rc;
     if (!d.h_ctx) {
@@ -1546,17 +1570,19 @@ int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* b
     call.eng = eng;
     call.host.assign(blocks, blocks + nblocks);
     call.slot.assign(nblocks, -1);
+    call.wr.reserve(nblocks);
     for (int id = 0; id < nblocks; id++) {
         if (upload[id]) {
             call.slot[id] = d.h_up;
-            memcpy(c.pinned + (size_t)d.h_up * pitch, blocks[id], (size_t)B);  // inputs read at call time
+            stream_copy(c.pinned + (size_t)d.h_up * pitch, blocks[id], (size_t)B);  // inputs read at call time
             d.h_up++;
         } else if (used[id]) {
             call.slot[id] = -2 - d.h_w++;
         }
         if (written[id]) {
             call.wr.push_back(id);
-            d.h_out[(uintptr_t)blocks[id]] = 1;
+            d.h_out.at(blocks[id]).wr = 1;
+            d.h_nout++;
             d.h_inplace |= upload[id] != 0;
         }
     }
@@ -1613,6 +1639,7 @@ int host_flush() {
         c.cap = total;
     }
     if (const int rc = ensure_pinned(c, total, a_bytes); rc != ECG_OK) return fail(rc);
+    _mm_sfence();  // the region's non-temporal stores (stream_copy) are globally visible before the DMA reads it
     if (a_bytes && hipMemcpyAsync(c.scratch, c.pinned, a_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
         set_last_error("hipMemcpyAsync(host batch H2D) failed");
         return fail(ECG_EHIP);
