@@ -652,9 +652,9 @@ struct DeferScope {
     std::vector<HostCall> hq;
     int h_up = 0, h_w = 0;
     long long h_B = -1;
-    bool h_inplace = false;                  // a written block has a region-A slot (read, then written)
-    PtrGroups h_out;                           // pending output block addresses (wr = 1), open addressing
-    size_t h_nout = 0;
+    bool h_inplace = false;  // a written block has a region-A slot (read, then written)
+    PtrGroups h_out;         // pending output block addresses (wr = 1), open addressing
+    size_t h_nout = 0;       // entries in h_out (a block is written at most once per batch: a second write flushes)
     std::unique_ptr<CtxLease> h_ctx;
     ~DeferScope() { release_order_evs(); }
 };
