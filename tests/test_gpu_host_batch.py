@@ -158,3 +158,45 @@ def test_deferred_host_mixed_with_device_calls_and_large_blocks(ecg, oracle, tor
 
 def test_defer_host_outside_scope_refused(ecg, torch_cuda):
     assert ecg.lib().ecg_batch_defer_host(1) != 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_deferred_host_random_sequences_match_sequential(ecg, oracle, torch_cuda, seed):
+    """Random host-tier call sequences over a small pool of shared buffers, so that calls read blocks an
+    earlier call of the scope writes (the scope must flush first), overwrite blocks an earlier call read
+    (its inputs were staged at call time), write a block twice, change block size mid-scope, flush
+    explicitly, and run dotprods and region XORs between encodes.  The GF arithmetic of every call is the
+    oracle's (jerasure_matrix_encode / dotprod restated).  The pool after the scope must equal the
+    oracle applying the same calls one by one."""
+    rng = np.random.default_rng(seed)
+    sizes = (1024, 4112) if seed % 2 else (64, 2048)
+    pools = {B: [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(12)] for B in sizes}
+    ref = {B: [x.copy() for x in pool] for B, pool in pools.items()}
+    with ecg.batch(host=True) as b:
+        for i in range(160):
+            B = sizes[int(rng.integers(0, 4)) == 0]  # mostly the first size: block-size changes flush
+            pool, rp = pools[B], ref[B]
+            kind = int(rng.integers(0, 10))
+            if kind < 7:  # encode: k data blocks -> m coding blocks, all distinct
+                k, m = int(rng.integers(1, 7)), int(rng.integers(1, 4))
+                ids = rng.choice(len(pool), size=k + m, replace=False).tolist()
+                M = [int(x) for x in rng.integers(0, 256, k * m)]
+                assert ecg.jerasure_matrix_encode(k, m, M, [pool[j] for j in ids[:k]],
+                                                  [pool[j] for j in ids[k:]], B) == 0
+                oracle.jerasure_matrix_encode(k, m, M, [rp[j] for j in ids[:k]], [rp[j] for j in ids[k:]], B)
+            elif kind < 9:  # dotprod into one block
+                k = int(rng.integers(1, 6))
+                ids = rng.choice(len(pool), size=k + 1, replace=False).tolist()
+                row = [int(x) for x in rng.integers(1, 256, k)]
+                assert ecg.jerasure_matrix_dotprod(k, row, None, k, [pool[j] for j in ids[:k]],
+                                                   [pool[ids[k]]], B) == 0
+                oracle.jerasure_matrix_dotprod(k, row, None, k, [rp[j] for j in ids[:k]], [rp[ids[k]]], B)
+            elif kind < 10 and i % 2:  # region XOR (host regions: flushes the pending calls first)
+                src, dst = rng.choice(len(pool), size=2, replace=False).tolist()
+                assert ecg.galois_region_xor(pool[src], pool[dst], B) == 0
+                rp[dst] ^= rp[src]
+            else:
+                b.flush()
+    for B in sizes:
+        for j, (a, r) in enumerate(zip(pools[B], ref[B])):
+            assert np.array_equal(a, r), (seed, B, j)
