@@ -1547,8 +1547,10 @@ int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* b
         if (const int rc = batch_flush(); rc != ECG_OK) return rc;  // at most one queue holds calls
     bool flush = !d.hq.empty() && (d.h_B != B || d.hq.back().eng != eng ||
                                    (size_t)(d.h_up + d.h_w + nup + nw) * pitch > kHostDeferMaxBytes);
+#ifndef ECG_TEST_NO_HOST_HAZARD_FLUSH  // test hook: a variant without this flush must fail the random-sequence test
     for (int id = 0; id < nblocks && !flush && d.h_nout; id++)
         flush = used[id] && d.h_out.last_write(blocks[id]) > 0;
+#endif
     if (flush)
         if (const int rc = host_flush(); rc != ECG_OK) return rc;
     if (!d.h_ctx) {
