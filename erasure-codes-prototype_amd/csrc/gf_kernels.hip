@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
 // bytes per lane the same bytes are 256 lanes in 4 waves on 4 SIMDs, each with a quarter of the multiply.
 // KB = the input count rounded up to a bucket (k <= KB): straight-line code over KB inputs, every input
 // load in flight at once.  Padded inputs (u >= k) re-read input 0 with table 0 and are masked out of the sum.
-// kLatThreads dword columns per workgroup; grid.x = ceil((B / 4) / kLatThreads), grid.y = row tiles.
+// kLatThreads dword columns per workgroup; grid.x = ceil((B / 4) / kLatThreads), one row tile (m <= kMaxMT).
 //
 // Coefficient tables through LDS (round 4).  The row tile's k * MT tables are k * MT * 5 dwords: 200 for
 // RS(10,4), more than the SGPR file holds, so as scalar loads they came in ~40 dependent rounds of
@@ -317,9 +317,26 @@ struct LatTabs {
     CoefTab t[kLatThreads / 64][KB * MT];                   // one slice per wave
 };
 
+// The latency kernel's own argument block (round 5).  A single call's launch is host-bound: the runtime
+// writes the kernel arguments into device-visible memory per launch, and a back-to-back launch costs 2.74 us
+// of host time with 24 bytes of arguments against 3.51 us with GfLaunch's 1432 (launch_floor_host_run*.txt,
+// profiles/r04/lat_tables/).  LatArgs carries only what the kernel reads -- KB input and MT output pointers
+// (80 bytes for config 3's 4 -> 1 bucket, 232 for the largest) -- and takes one row tile (m <= kMaxMT; wider
+// single calls run gf_vec_kernel).
+template <int KB, int MT>
+struct LatArgs {
+    const CoefTab* tabs;  // [k][MT]
+    unsigned* done_flags;
+    long long B;
+    int k, m;
+    unsigned done_seq;
+    const uint8_t* src[KB];  // slots u >= k repeat input 0
+    uint8_t* dst[MT];        // slots p >= m repeat output 0 (never stored)
+};
+
 template <int MT, int KB>
-__device__ __forceinline__ void lat_tabs_load(const GfLaunch& a, int rt, u32x4 (&tv)[LatTabs<MT, KB>::kPerLane]) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.tabs + (size_t)rt * (size_t)a.k * MT);
+__device__ __forceinline__ void lat_tabs_load(const LatArgs<KB, MT>& a, u32x4 (&tv)[LatTabs<MT, KB>::kPerLane]) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.tabs);
     const int last = a.k * MT * 2 - 1;  // this tile's last piece (k <= KB)
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -393,28 +410,24 @@ __device__ __forceinline__ void lat_fold_lds(const int k, const CoefTab* T, cons
 // Every lane runs the whole body: lanes past the end load the last column and store nothing, so no branch
 // precedes the loads and a wave past the end still reaches the flag epilogue.
 template <int MT, bool BIN, int KB, bool EAGER>
-__global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLaunch a) {
+__global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const LatArgs<KB, MT> a) {
     __shared__ LatTabs<MT, KB> lds;
-    const int rt = blockIdx.y;
     const int k = a.k;
-    const int row0 = rt * MT;
-    const int nrows = min(MT, a.m - row0);
+    const int nrows = a.m;
     const long long ndw = a.B >> 2;
     const long long c = (long long)blockIdx.x * kLatThreads + threadIdx.x;
-    // Every input pointer slot is read with a constant index and then selected (a.isrc has kInlineSrc >= KB
-    // slots, the unused ones zeroed): one round of kernel-argument loads, no address computed from k.
+    // Every pointer slot is read with a constant index (the host filled the padded slots): one round of
+    // kernel-argument loads, no address computed from k; the flag word in the same round (not after the fold).
     const uint8_t* src[KB];
 #pragma unroll
-    for (int u = 0; u < KB; ++u) src[u] = a.isrc[u];
+    for (int u = 0; u < KB; ++u) src[u] = a.src[u];
+    uint8_t* dst[MT];
 #pragma unroll
-    for (int u = 1; u < KB; ++u) src[u] = u < k ? src[u] : src[0];
-    uint8_t* dst[MT];  // the output pointers and the flag word in the same round (not after the fold)
-#pragma unroll
-    for (int p = 0; p < MT; ++p) dst[p] = a.idst[min(row0 + p, kInlineDst - 1)];
+    for (int p = 0; p < MT; ++p) dst[p] = a.dst[p];
     unsigned* const flags = a.done_flags;
     // the table loads go out first
     u32x4 tv[LatTabs<MT, KB>::kPerLane];
-    lat_tabs_load<MT, KB>(a, rt, tv);
+    lat_tabs_load<MT, KB>(a, tv);
     __builtin_amdgcn_sched_barrier(0);
     const bool live = c < ndw;
     const long long off = (live ? c : ndw - 1) << 2;
@@ -430,7 +443,7 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const GfLa
         for (int p = 0; p < MT; ++p)
             if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(dst[p] + off));
     }
-    if (flags) post_done_flag(flags + blockIdx.y * gridDim.x + blockIdx.x, a.done_seq);
+    if (flags) post_done_flag(flags + blockIdx.x, a.done_seq);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -733,8 +746,17 @@ Launcher pick_vec(const GfLaunch& a, int nt) {
 
 template <int MT, bool BIN, int KB>
 hipError_t lat_dword_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
-    if (a.B <= kLatEagerBytes) return launch_kernel(gf_lat_dword_kernel<MT, BIN, KB, true>, g, dim3(kLatThreads), st, a);
-    return launch_kernel(gf_lat_dword_kernel<MT, BIN, KB, false>, g, dim3(kLatThreads), st, a);
+    LatArgs<KB, MT> l;
+    l.tabs = a.tabs;
+    l.done_flags = a.done_flags;
+    l.B = a.B;
+    l.k = a.k;
+    l.m = a.m;
+    l.done_seq = a.done_seq;
+    for (int u = 0; u < KB; ++u) l.src[u] = a.isrc[u < a.k ? u : 0];
+    for (int p = 0; p < MT; ++p) l.dst[p] = a.idst[p < a.m ? p : 0];
+    if (a.B <= kLatEagerBytes) return launch_kernel(gf_lat_dword_kernel<MT, BIN, KB, true>, g, dim3(kLatThreads), st, l);
+    return launch_kernel(gf_lat_dword_kernel<MT, BIN, KB, false>, g, dim3(kLatThreads), st, l);
 }
 
 // input-count buckets of the latency kernel: exact for the BASELINE shapes (RS(6,4), RS(10,4) encode and
@@ -837,14 +859,14 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
     GfLaunch a = base;
     const long long vec_bytes = vec_ok ? (a.B & ~15LL) : 0;
     if (mode == GF_MODE_INLINE_LAT && vec_bytes == a.B && a.B <= g_opt[ECG_OPT_LAT_DWORD_BYTES].load() &&
-        a.k <= kLatMaxSrc) {
+        a.k <= kLatMaxSrc && a.rtiles == 1) {
         // small zero-copy call: 4 bytes per lane (gf_lat_dword_kernel)
         const long long gx = ((a.B >> 2) + kLatThreads - 1) / kLatThreads;
         Launcher l = a.binary ? pick_lat_dword_bin<true>(a.MT, a.k) : pick_lat_dword_bin<false>(a.MT, a.k);
         if (!l) return hipErrorInvalidValue;
-        const hipError_t e = l(a, dim3((unsigned)gx, (unsigned)a.rtiles), st);
+        const hipError_t e = l(a, dim3((unsigned)gx), st);
         if (e != hipSuccess) return e;
-        if (n_wg) *n_wg = (int)(gx * a.rtiles);
+        if (n_wg) *n_wg = (int)gx;
         return hipSuccess;
     }
     if (vec_bytes > 0) {
