@@ -105,6 +105,10 @@ def parse():
     ap.add_argument("--config5-block-size", type=int, default=CONFIG5_BLOCK)
     ap.add_argument("--no-host-path", action="store_true",
                     help="default workload: skip the host-path sub-object (pinned host batch incl. PCIe copies)")
+    ap.add_argument("--no-configs34", action="store_true",
+                    help="default workload: skip the config3 / config4 sub-objects (LRC repair, PC merge on one GPU)")
+    ap.add_argument("--configs34-stripes", type=int, default=None,
+                    help="default workload: stripes (config 3) / merges (config 4) per GPU (default 4096 / 512)")
     ap.add_argument("--ring-scale", type=float, default=1.0,
                     help="default workload: scale the cross-GPU objects' stripe / merge counts (rehearsals of many "
                          "ranks on one GPU)")
@@ -429,16 +433,186 @@ def rs_encode_decode(a, r):
             line["config5"] = config5(a, r, M, k, m)
         if not a.no_host_path:
             line["host_path"] = host_path_line(a, r, M, k, m)
+        if not a.no_configs34:
+            line["config3"] = config3_line(a, r)
+            line["config4"] = config4_line(a, r)
         if not a.no_ring:
             sc = lambda n: max(8, int(n * a.ring_scale)) // 8 * 8  # noqa: E731
             line["ring_repair"] = ring_repair_line(a, r, S=sc(1024))
             line["global_ring_repair"] = ring_repair_line(a, r, S=sc(256), glob=True)
             line["merge_ring"] = merge_ring_line(a, r, S=sc(64))
 
-    optional_section(line, r, ["config5", "host_path", "ring_repair", "global_ring_repair", "merge_ring"], optional)
+    optional_section(line, r, ["config5", "host_path", "config3", "config4", "ring_repair", "global_ring_repair",
+                               "merge_ring"], optional)
     if r.world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(k, m, B, a.cpu_seconds)
     return line
+
+
+# ------------------------------------------------------------------------------- configs 3 and 4 in the line
+
+WORKLOAD_PROFILE = os.path.join(ROOT, "profiles", "workload_profile.json")
+CONFIG3_FORMS = ("fused", "reference_sequence_scope_scratch", "reference_sequence_per_call",
+                 "reference_sequence_per_call_threads8")
+CONFIG4_FORMS = ("rows", "fused")
+
+
+def workload_profile(key):
+    """The committed rocprofv3 kernel-trace summary of one form (tools/workload_profile.py ->
+    profiles/workload_profile.json): its dominant kernel, that kernel's average launch, the kernels' busy
+    time per batch, and whether it was taken on this libecg.so build."""
+    try:
+        prof = json.load(open(WORKLOAD_PROFILE))
+        f = prof["forms"][key]
+        return {"kernel": f["dominant_kernel"], "profile_kernel_avg_us": f["dominant_avg_us"],
+                "profile_kernel_launches_per_batch": f["dominant_launches_per_batch"],
+                "profile_kernel_busy_ms_per_batch": f["kernel_busy_ms_per_batch"],
+                "profile_kernel_busy_frac": f["kernel_busy_frac"],
+                "profile_source": "profiles/workload_profile.json <- " + f["source"],
+                "profile_is_this_build": prof["libecg_sha16"] == libecg_sha16()}
+    except Exception:  # noqa: BLE001 -- no committed profile for this form: the object says so
+        return {"kernel": None, "profile_source": None}
+
+
+def seq_cpu_baseline(nb, nout, B, patterns, pat_of, target_s, nscr, S, fill=None):
+    """The oracle's CPU restatement of a per-stripe call sequence (ref.call_seq_batch_mt: every call one
+    jerasure_matrix_encode with the SIMD split-table region kernels) on a bounded sample of S stripes,
+    repeated for about target_s seconds, one worker thread per host CPU this process may use.  Returns
+    (seconds, repetitions, threads, host facts, stripes, out)."""
+    import numpy as np
+    from oracle import ref
+    ref.build()
+    threads, facts = host_cpus()
+    stripes = ref.splitmix_bytes(0xEC0DE, 0, S * nb * B).reshape(S, nb, B)
+    if fill is not None:
+        fill(stripes)
+    out = np.zeros((S, nout, B), np.uint8)
+    reps, t_total = 0, 0.0
+    while t_total < target_s and reps < 1000:
+        t0 = time.perf_counter()
+        rc = ref.call_seq_batch_mt(stripes, out, patterns, pat_of, nscr, threads)
+        t_total += time.perf_counter() - t0
+        reps += 1
+        if rc < 0:
+            raise RuntimeError("oracle call_seq_batch_mt failed")
+    return t_total, reps, threads, facts, stripes, out
+
+
+def config3_line(a, r):
+    """BASELINE.json configs[2] in the default line: Azure-LRC(12,2,2), 1 MiB, single-block repair of block
+    s mod 16 of each of 4096 stripes per GPU with partial decoding (lrc_repair): the fused form, the
+    reference's per-stripe call sequence (help_repair's partial, main_repair's partial, perform_addition;
+    handle_repair.cpp:246-252,370-376) in batch scopes with the partials declared scratch, and the same
+    sequence one call at a time from 1 and 8 host threads.  Each form: HIP-event time, algorithmic and
+    executed bytes, the committed profile's kernel, every repaired block verified.  Rank 0 at N = 1 adds the
+    oracle's CPU run of the same per-stripe calls."""
+    try:
+        torch.cuda.empty_cache()
+        res = lrc_repair(a, r, only=CONFIG3_FORMS, steps=min(a.steps, 10), warmup=min(a.warmup, 2),
+                         S=a.configs34_stripes or 4096, B=1 << 20)
+        out = {"workload": "Azure-LRC(12,2,2) single-block repair (block s mod 16), partial_decoding=true, 1 MiB, "
+                           f"{res['stripes_per_gpu']} stripes per GPU (BASELINE configs[2])",
+               "algorithmic_bytes_per_repair": "(survivors + 1) * B: 7 MiB local, 13 MiB global",
+               "algorithmic_bytes_per_batch": res["algorithmic_bytes_per_batch"],
+               "local_repairs": res["local_repairs"], "global_repairs": res["global_repairs"], "forms": {}}
+        for name, v in res["results"].items():
+            out["forms"][name] = {**v, **workload_profile(f"config3/{name}")}
+        del res
+        torch.cuda.empty_cache()
+        if r.world == 1 and r.rank == 0 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = config3_cpu_baseline(a)
+        return out
+    except Exception as e:  # noqa: BLE001 -- reported, the headline stands
+        return {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+
+
+def config3_cpu_baseline(a):
+    """The reference's per-stripe repair calls on the CPU over 1 MiB blocks: a local repair is the helper
+    partial, the main partial and perform_addition (three jerasure_matrix_encode calls, 1 x 3, 1 x 3, 1 x 2);
+    a global-parity repair re-encodes its row from the 12 data blocks.  Stripe s repairs block s mod 16."""
+    import numpy as np
+    from oracle import ref
+    k, g, l, B = 12, 2, 2, 1 << 20
+    n = k + g + l
+    cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
+    ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)
+    ec.init_coding_parameters(cp)
+    M = ec.make_encoding_matrix()
+    patterns = []
+    for e in range(n):
+        if e in (12, 13):
+            patterns.append([(n, list(range(k)), M[(e - 12) * k:(e - 11) * k])])
+            continue
+        surv, sets = azure_local_split(e)
+        h = ec.partial_decoding_matrix(sets[0], surv, [e])
+        mn = ec.partial_decoding_matrix(sets[1], surv, [e])
+        patterns.append([(n + 1, sets[0], h), (n + 2, sets[1], mn), (n, [n + 1, n + 2], [1, 1])])
+    threads, _ = host_cpus()
+    S = 2 * n * max(1, (2 * threads + n - 1) // n)  # whole rounds of the 16 patterns, >= 2 per thread
+    pat_of = np.arange(S, dtype=np.int32) % n
+
+    def encode(st):  # the stripes' parities (the repairs read them)
+        for s_ in range(st.shape[0]):
+            ref.jerasure_matrix_encode_simd(k, g + l, M, [st[s_, j] for j in range(k)],
+                                            [st[s_, j] for j in range(k, n)], B)
+
+    t, reps, threads, facts, stripes, out = seq_cpu_baseline(n, 1, B, patterns, pat_of, a.cpu_seconds / 4, 2, S,
+                                                             fill=encode)
+    local = sum(1 for s_ in range(S) if s_ % n not in (12, 13))
+    alg = (local * 7 + (S - local) * 13) * B
+    idx = np.arange(S)
+    return {"value": round(reps * alg / t / 1e9, 3), "unit": "GB/s of algorithmic bytes ((survivors + 1) * B per repair)",
+            "repairs_per_s": round(reps * S / t, 1), "cores": threads, "kind": "port", "threads_used": threads,
+            **facts, "verified": bool(np.array_equal(out[:, 0], stripes[idx, idx % n])),
+            "sample": f"{reps} x {S} repairs (block s mod 16), the reference's per-stripe calls (helper partial, "
+                      f"main partial, perform_addition; global rows re-encoded), {threads} host threads, {t:.1f} s"}
+
+
+def config4_line(a, r):
+    """BASELINE.json configs[3] in the default line: PC(4,1,4,1), 4 MiB blocks, stripe merging x = 2
+    (HORIZONTAL), 512 merges per GPU (pc_merge): the row form (each merged row parity one 8 -> 1 XOR launch
+    stripe) and the fused 40 -> 5 call the engine splits into rows.  Rank 0 at N = 1 adds the oracle's CPU
+    run of the same row calls."""
+    try:
+        torch.cuda.empty_cache()
+        res = pc_merge(a, r, only=CONFIG4_FORMS, steps=min(a.steps, 10), warmup=min(a.warmup, 2),
+                       S=a.configs34_stripes // 8 if a.configs34_stripes else 512, B=4 << 20)
+        out = {"workload": f"PC(4,1,4,1) merge x=2 horizontal, 4 MiB blocks, {res['merges_per_gpu']} merges per GPU: "
+                           "the 5 row parities of the merged PC(8,1,4,1) (BASELINE configs[3])",
+               "algorithmic_bytes_per_merge": "5 rows x 9 B = 180 MiB",
+               "algorithmic_bytes_per_batch": res["algorithmic_bytes_per_batch"], "forms": {}}
+        for name, v in res["results"].items():
+            out["forms"][name] = {**v, **workload_profile(f"config4/{name}")}
+        del res
+        torch.cuda.empty_cache()
+        if r.world == 1 and r.rank == 0 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = config4_cpu_baseline(a)
+        return out
+    except Exception as e:  # noqa: BLE001 -- reported, the headline stands
+        return {"error": f"{type(e).__name__}: {str(e)[:300]}"}
+
+
+def config4_cpu_baseline(a):
+    """The same merges on the CPU: per merge, 5 calls jerasure_matrix_encode(8, 1, all ones) over the row's
+    8 blocks of the two old stripes (blocks [2][25] per merge, PC(4,1,4,1) rowcol2bid, pc.cpp:326-340)."""
+    import numpy as np
+    B, nb = 4 << 20, 50
+
+    def bid(row, col):
+        return row * 4 + col if row < 4 else 20 + col
+    calls = [(nb + row, [half * 25 + bid(row, col) for half in range(2) for col in range(4)], [1] * 8)
+             for row in range(5)]
+    threads, _ = host_cpus()
+    S = 2 * threads
+    t, reps, threads, facts, blocks, out = seq_cpu_baseline(nb, 5, B, [calls], None, a.cpu_seconds / 4, 0, S)
+    ok = True
+    for row, (_, src, _) in enumerate(calls):
+        ok &= bool(np.array_equal(out[:, row], np.bitwise_xor.reduce(blocks[:, src], axis=1)))
+    return {"value": round(reps * S * 45 * B / t / 1e9, 3), "unit": "GB/s of algorithmic bytes (9 * B per row)",
+            "merges_per_s": round(reps * S / t, 1), "cores": threads, "kind": "port", "threads_used": threads,
+            **facts, "verified": ok,
+            "sample": f"{reps} x {S} merges (5 row calls jerasure_matrix_encode(8, 1, ones) each), {threads} host "
+                      f"threads, {t:.1f} s"}
 
 
 def optional_deadline_s() -> float:
@@ -561,16 +735,19 @@ def rs_decode_patterns(a, r):
 
 # ------------------------------------------------------------------------------- config 3
 
-def lrc_repair(a, r):
+def lrc_repair(a, r, only=None, steps=None, warmup=None, S=None, B=None):
     """Azure-LRC(12,2,2), 1 MiB: every stripe loses block e = s mod 16 and repairs it.
     Data / local-parity loss: local group of 6 survivors.  partial_decoding=true mirrors
     help_repair/main_repair (handle_repair.cpp:249,375,566): helper partial over the survivors in the
     helper partition, main partial over the rest, perform_addition of the two.  The fused form computes
     the repaired block in one launch from the same survivors.  Global-parity loss (12, 13): the global
-    path, re-encode from the 12 data blocks (jerasure_matrix_decode re-encodes erased coding rows)."""
+    path, re-encode from the 12 data blocks (jerasure_matrix_decode re-encodes erased coding rows).
+    only: the forms to run (default: --forms, else all); steps / warmup: per form (default: --steps / --warmup)."""
+    steps = a.steps if steps is None else steps
+    warmup = a.warmup if warmup is None else warmup
     k, l, g = 12, 2, 2
-    B = a.block_size or (1 << 20)
-    S = a.stripes or 4096
+    B = B or a.block_size or (1 << 20)
+    S = S or a.stripes or 4096
     n = k + g + l
     cp = ecg.CodingParameters(k=k, l=l, g=g, local_or_column=True)
     ec = ecg.ec_factory(ecg.ECTYPE.AZURE_LRC, cp)
@@ -708,26 +885,32 @@ def lrc_repair(a, r):
     results = {}
     n_local, n_glob = sl.numel(), sg.numel()
     alg = (n_local * 7 + n_glob * 13) * B  # (survivors + 1) * B per repair
-    forms = (("partial_decoding", step_partial, (n_local * (4 + 4 + 3) + n_glob * 13) * B),
-             ("partial_decoding_fused_main", step_fused_main, (n_local * (4 + 5) + n_glob * 13) * B),
-             ("fused", step_fused, alg),
-             ("reference_sequence_per_call", replay(0), (n_local * (4 + 4 + 3) + n_glob * 13) * B),
-             ("reference_sequence_scope", replay(1), (n_local * (4 + 4 + 3) + n_glob * 13) * B),
-             ("reference_sequence_scope_scratch", replay(2), None),
-             *((f"reference_sequence_per_call_threads{t}", replay_threads(t),
-                (n_local * (4 + 4 + 3) + n_glob * 13) * B) for t in REPLAY_THREADS))
-    if a.forms:
-        forms = tuple(f for f in forms if f[0] in a.forms.split(","))
-    for name, fn, executed in forms:
+    per_call_bytes = (n_local * (4 + 4 + 3) + n_glob * 13) * B  # the partials round-trip HBM
+    # (name, form factory -- built only when the form runs, executed bytes per batch)
+    forms = (("partial_decoding", lambda: step_partial, per_call_bytes),
+             ("partial_decoding_fused_main", lambda: step_fused_main, (n_local * (4 + 5) + n_glob * 13) * B),
+             ("fused", lambda: step_fused, alg),
+             ("reference_sequence_per_call", lambda: replay(0), per_call_bytes),
+             ("reference_sequence_scope", lambda: replay(1), per_call_bytes),
+             ("reference_sequence_scope_scratch", lambda: replay(2), None),
+             *((f"reference_sequence_per_call_threads{t}", (lambda t=t: replay_threads(t)), per_call_bytes)
+               for t in REPLAY_THREADS))
+    wanted = only if only is not None else (a.forms.split(",") if a.forms else None)
+    if wanted is not None:
+        forms = tuple(f for f in forms if f[0] in wanted)
+    for name, make, executed in forms:
+        fn = make()
         rebuilt.zero_()
-        for _ in range(a.warmup):
+        for _ in range(warmup):
             fn()
         torch.cuda.synchronize()
         assert torch.equal(rebuilt[:, 0], stripes[idx, e_of.long()]), f"{name}: repair mismatch"
-        elapsed, evs = timed_loop(r, a.steps, fn)
+        elapsed, evs = timed_loop(r, steps, fn)
         t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
-        res = {"repairs_per_s": round(r.world * S * a.steps / elapsed, 1), "ms_per_batch": round(t * 1e3, 3),
-               "algorithmic_GBps": round(alg / t / 1e9, 1), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+        res = {"repairs_per_s": round(r.world * S * steps / elapsed, 1), "ms_per_batch": round(t * 1e3, 3),
+               "algorithmic_GBps": round(alg / t / 1e9, 1), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+               "verified": True,  # every repaired block equal to the lost one (the assert above)
+               "batches_run": warmup + steps}
         if name == "reference_sequence_scope_scratch":
             st = replay_stats[2]  # the last scope's flush: 3 recorded calls per repair, composed to 1
             res["last_scope_flush"] = st
@@ -744,9 +927,12 @@ def lrc_repair(a, r):
                                    "stream over a contiguous share of the repairs")
         res["executed_bytes_per_batch"] = executed
         res["executed_GBps"] = round(executed / t / 1e9, 1) if executed else None
+        res["executed_frac"] = round(executed / t / 1e9 / HBM_PEAK_GBS, 4) if executed else None
         results[name] = res
+        del fn
     return {"workload": "Azure-LRC(12,2,2) single-block repair, block s mod 16, 1 MiB", "n_gpus": r.world,
-            "stripes_per_gpu": S, "steps": a.steps, "results": results, "dtype": "u8",
+            "stripes_per_gpu": S, "steps": steps, "local_repairs": n_local, "global_repairs": n_glob,
+            "algorithmic_bytes_per_batch": alg, "results": results, "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
@@ -968,13 +1154,16 @@ def lrc_repair_ring(a, r):
 
 # ------------------------------------------------------------------------------- config 4
 
-def pc_merge(a, r):
+def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
     """PC(4,1,4,1), 4 MiB blocks, merge x=2 HORIZONTAL: merged PC(8,1,4,1) row r parity = XOR of the
     two old stripes' row-r data blocks (r < 4) / column-parity blocks (r = 4); the RS(8,1) row code is all
     ones (main_recal / help_recal, handle_merge.cpp:159,269,319,453).  One launch reads 40 blocks and
-    writes 5 per merge (the algorithmic minimum, 9 * B per row).  Two formulations are timed (below)."""
-    B = a.block_size or (4 << 20)
-    S = a.stripes or 512
+    writes 5 per merge (the algorithmic minimum, 9 * B per row).  Three formulations are timed (below);
+    only / steps / warmup as in lrc_repair."""
+    steps = a.steps if steps is None else steps
+    warmup = a.warmup if warmup is None else warmup
+    B = B or a.block_size or (4 << 20)
+    S = S or a.stripes or 512
     old = ecg.ec_factory(ecg.ECTYPE.PC, ecg.CodingParameters(k1=4, m1=1, k2=4, m2=1))
     nb = old.k + old.m  # 25 blocks per PC(4,1,4,1) stripe
     blocks = torch.empty((S, 2 * nb, B), dtype=torch.uint8, device="cuda")
@@ -1014,7 +1203,10 @@ def pc_merge(a, r):
     }
     alg = S * 45 * B
     res = {}
+    wanted = only if only is not None else (a.forms.split(",") if a.forms else None)
     for name, fn in variants.items():
+        if wanted is not None and name not in wanted:
+            continue
         def step(ev=None, fn=fn):
             if ev:
                 ev[0].record()
@@ -1023,7 +1215,7 @@ def pc_merge(a, r):
                 ev[1].record()
 
         out.zero_()
-        for _ in range(a.warmup):
+        for _ in range(warmup):
             step()
         torch.cuda.synchronize()
         for s in (0, S // 2 + 1, S - 1):  # merges checked against XOR on the host
@@ -1034,13 +1226,27 @@ def pc_merge(a, r):
                     for col in range(4):
                         x = hb[half * nb + bid(row, col)] ^ x
                 assert (out[s, row].cpu().numpy() == x).all(), f"merge mismatch ({name})"
-        elapsed, evs = timed_loop(r, a.steps, step)
+        # every merge of the batch against the XOR of its blocks, on the GPU (the host check above is
+        # independent of torch's XOR; this one covers all S merges)
+        ok = True
+        for s0 in range(0, S, 32):
+            s1 = min(S, s0 + 32)
+            for row in range(5):
+                x = blocks[s0:s1, src[8 * row]].clone()
+                for j in src[8 * row + 1:8 * row + 8]:
+                    x ^= blocks[s0:s1, j]
+                ok &= bool(torch.equal(out[s0:s1, row], x))
+            del x
+        assert ok, f"merge mismatch ({name}, device check)"
+        elapsed, evs = timed_loop(r, steps, step)
         t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
-        res[name] = {"ms_per_batch": round(t * 1e3, 3), "merges_per_s": round(r.world * S * a.steps / elapsed, 1),
+        res[name] = {"ms_per_batch": round(t * 1e3, 3), "merges_per_s": round(r.world * S * steps / elapsed, 1),
                      "algorithmic_GBps": round(alg / t / 1e9, 1),
-                     "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+                     "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                     "executed_bytes_per_batch": alg, "executed_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                     "verified": True, "batches_run": warmup + steps}
     return {"workload": "PC(4,1,4,1) merge x=2 horizontal, 4 MiB blocks", "n_gpus": r.world,
-            "merges_per_gpu": S, "steps": a.steps, "results": res,
+            "merges_per_gpu": S, "steps": steps, "algorithmic_bytes_per_batch": alg, "results": res,
             "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
 
 

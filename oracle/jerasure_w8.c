@@ -606,3 +606,77 @@ int orc_decode_batch_mt(int k, int m, const int *matrix, uint8_t *stripes, uint8
 }
 
 int orc_have_avx2(void) { return have_avx2(); }
+
+/* ---------------------------------------------------------------- CPU baseline: call sequences */
+
+/* bench.py's config3 / config4 objects: per stripe, the proxies' calls as jerasure_matrix_encode(kin, 1, ...)
+   calls with the SIMD region kernels -- config 3: help_repair's partial, main_repair's partial and
+   perform_addition (handle_repair.cpp:246-252,370-376; erasure_code.cpp:70-94,113-150); config 4: one
+   all-ones row per merged parity (handle_merge.cpp:145-177,318-321).
+   stripes: [S][nb][B]; out: [S][nout][B]; stripe s runs pattern pat[s] (0 when pat is NULL).  Pattern p's
+   calls are packed in calls[off[p] .. off[p + 1]) as [kin, dst, src_0 .. src_{kin-1}, coef_0 .. coef_{kin-1}].
+   Block ids: 0 .. nb-1 the stripe's blocks, nb .. nb+nout-1 its out blocks, nb+nout .. nb+nout+nscr-1
+   per-thread scratch blocks (the partials, fresh per stripe as the proxy's std::vector<char>(B) are). */
+struct seq_arg {
+    const uint8_t *stripes;
+    uint8_t *out;
+    long nb, nout, B, s0, s1;
+    const int *pat, *off, *calls;
+    int nscr, rc;
+};
+
+static void *seq_worker(void *p)
+{
+    struct seq_arg *a = (struct seq_arg *)p;
+    uint8_t *scr = (uint8_t *)malloc((size_t)(a->nscr > 0 ? a->nscr : 1) * (size_t)a->B);
+    if (!scr) { a->rc = -1; return NULL; }
+    for (long s = a->s0; s < a->s1; s++) {
+        const int pt = a->pat ? a->pat[s] : 0;
+        for (int i = a->off[pt]; i < a->off[pt + 1];) {
+            const int kin = a->calls[i], dst = a->calls[i + 1];
+            const int *src = a->calls + i + 2, *coef = a->calls + i + 2 + kin;
+            uint8_t *in[256], *o[1];
+            long ids[257];
+            for (int j = 0; j <= kin; j++) ids[j] = j < kin ? src[j] : dst;
+            for (int j = 0; j <= kin; j++) {
+                const long id = ids[j];
+                uint8_t *b;
+                if (id < a->nb) b = (uint8_t *)a->stripes + ((size_t)s * a->nb + id) * a->B;
+                else if (id < a->nb + a->nout) b = a->out + ((size_t)s * a->nout + (id - a->nb)) * a->B;
+                else b = scr + (size_t)(id - a->nb - a->nout) * a->B;
+                if (j < kin) in[j] = b;
+                else o[0] = b;
+            }
+            orc_matrix_encode_simd(kin, 1, coef, in, o, a->B);
+            i += 2 + 2 * kin;
+        }
+    }
+    free(scr);
+    return NULL;
+}
+
+int orc_call_seq_batch_mt(const uint8_t *stripes, long nb, uint8_t *out, long nout, long B, long S, const int *pat,
+                          const int *off, const int *calls, int nscr, int nthreads)
+{
+    if (nthreads < 1) return -1;
+    ensure_tables();
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    struct seq_arg args[256];
+    long per = (S + nthreads - 1) / nthreads;
+    int used = 0;
+    for (int t = 0; t < nthreads; t++) {
+        long s0 = t * per, s1 = s0 + per;
+        if (s1 > S) s1 = S;
+        if (s0 >= s1) break;
+        args[t] = (struct seq_arg){stripes, out, nb, nout, B, s0, s1, pat, off, calls, nscr, 0};
+        pthread_create(&th[t], NULL, seq_worker, &args[t]);
+        used++;
+    }
+    int rc = used;
+    for (int t = 0; t < used; t++) {
+        pthread_join(th[t], NULL);
+        if (args[t].rc) rc = -1;
+    }
+    return rc;
+}

@@ -60,6 +60,7 @@ def lib():
         L.orc_matrix_decode.argtypes = [I, I, IP, I, IP, PP, PP, Lg]
         L.orc_encode_batch_mt.argtypes = [I, I, IP, P, P, Lg, Lg, I]
         L.orc_decode_batch_mt.argtypes = [I, I, IP, P, P, Lg, Lg, I]
+        L.orc_call_seq_batch_mt.argtypes = [P, Lg, P, Lg, Lg, Lg, P, IP, IP, I, I]
         _lib = L
     return _lib
 
@@ -154,6 +155,30 @@ def decode_batch_mt(k, m, matrix, stripes: np.ndarray, out: np.ndarray, B: int, 
     """CPU baseline: stripe s ([S][k+m][B]) loses block s mod (k+m), rebuilt into out[s] by one
     jerasure_matrix_decode (SIMD region kernels) per stripe over nthreads."""
     return lib().orc_decode_batch_mt(k, m, _ints(matrix), stripes.ctypes.data, out.ctypes.data, B, S, nthreads)
+
+
+def call_seq_batch_mt(stripes: np.ndarray, out: np.ndarray, patterns, pat_of_stripe, nscr: int, nthreads: int) -> int:
+    """CPU baseline of a per-stripe call sequence (bench.py config3 / config4): stripes [S][nb][B], out
+    [S][nout][B]; patterns[p] = [(dst, [src ids], [coefs]), ...], each call one jerasure_matrix_encode(kin, 1)
+    (SIMD region kernels).  Ids: stripe blocks 0..nb-1, out blocks nb.., then nscr per-thread scratch
+    blocks.  Stripe s runs patterns[pat_of_stripe[s]] (pattern 0 when pat_of_stripe is None)."""
+    S, nb, B = stripes.shape
+    nout = out.shape[1]
+    assert out.shape[0] == S and out.shape[2] == B and stripes.flags["C_CONTIGUOUS"] and out.flags["C_CONTIGUOUS"]
+    off, packed = [0], []
+    for calls in patterns:
+        for dst, src, coef in calls:
+            assert len(src) == len(coef) and 0 < len(src) <= 256
+            assert all(0 <= i < nb + nout + nscr for i in list(src) + [dst])
+            packed += [len(src), dst, *src, *coef]
+        off.append(len(packed))
+    pat = None
+    if pat_of_stripe is not None:
+        pat = np.ascontiguousarray(pat_of_stripe, dtype=np.int32)
+        assert pat.shape == (S,) and pat.min() >= 0 and pat.max() < len(patterns)
+    return lib().orc_call_seq_batch_mt(stripes.ctypes.data, nb, out.ctypes.data, nout, B, S,
+                                       pat.ctypes.data if pat is not None else None, _ints(off), _ints(packed),
+                                       nscr, nthreads)
 
 
 # ------------------------------------------------------------------ synthetic data (SURVEY.md §8(d))

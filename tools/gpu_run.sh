@@ -17,6 +17,12 @@
 #   wprof      rocprofv3 kernel stats of each non-default workload
 #   w:<name>   one workload line                                                  -> bench_<name>.log
 #   wp:<name>  rocprofv3 kernel stats of one workload
+#   w34prof    rocprofv3 kernel traces of each form the line's config3 / config4 objects time (one run per
+#              form) -> workload_profile.json (tools/workload_profile.py; copy it to profiles/ for bench.py)
+#   ceiling    tools/movement_ceiling: the product kernel's own access path with the multiply removed, and its
+#              rocprofv3 kernel stats                                             -> ceiling.txt, ceiling_prof/
+#   abrepair   config 3's per-call forms (1 and 8 threads), the tree's libecg vs lib/ab/ (ECG_LIB), alternated
+#              over 3 rounds                                                       -> abrepair_<v>_<r>.log
 #   callrate   tools/call_rate + tools/record_cost (device-tier per-call cost)     -> call_rate.txt, record_cost.txt
 #   ab         per-call cost A/B: the tree's libecg vs erasure-codes-prototype_amd/lib/ab/ (a build of an earlier
 #              commit), tools/call_rate device + tools/record_cost, alternated over 3 rounds -> ab_<v>_<r>.txt
@@ -89,6 +95,33 @@ for step in "$@"; do
     w:*) w=${step#w:}; run "bench $w" 500 "$O/bench_$w.log" python bench.py --workload $w --no-cpu-baseline
          tail -1 "$O/bench_$w.log" | cut -c1-600 ;;
     wp:*) w=${step#wp:}; prof "wprof/$w" "wprof_$w.log" --workload $w --no-cpu-baseline ;;
+    w34prof) C3="fused reference_sequence_scope_scratch reference_sequence_per_call reference_sequence_per_call_threads8"
+             C4="rows fused"
+             spec=""
+             for f in $C3; do
+               prof "w34/c3_$f" "w34_c3_$f.log" --workload lrc-repair --forms $f --steps 10 --warmup 2 --no-cpu-baseline
+               spec="$spec config3/$f=$O/w34/c3_$f/run_kernel_trace.csv:$O/w34_c3_$f.log:$f"
+             done
+             for f in $C4; do
+               prof "w34/c4_$f" "w34_c4_$f.log" --workload pc-merge --forms $f --steps 10 --warmup 2 --no-cpu-baseline
+               spec="$spec config4/$f=$O/w34/c4_$f/run_kernel_trace.csv:$O/w34_c4_$f.log:$f"
+             done
+             python tools/workload_profile.py "$O/workload_profile.json" $spec > "$O/workload_profile.log" 2>&1 \
+               && echo "workload_profile ok" || exit 1 ;;
+    ceiling) run ceiling 200 "$O/ceiling.txt" ./tools/movement_ceiling 4 10
+             (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$O/ceiling_prof" -o run \
+                --output-format csv -- "$R/tools/movement_ceiling" 2 10 > "$R/$O/ceiling_prof.txt" 2>&1)
+             rc=$?; echo "ceiling prof rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    abrepair) for r in 1 2 3; do
+                for v in new prev; do
+                  if [ $v = prev ]; then EL=$R/erasure-codes-prototype_amd/lib/ab/libecg.so; else EL=$R/erasure-codes-prototype_amd/lib/libecg.so; fi
+                  run "lrc per-call $v $r" 300 "$O/abrepair_${v}_$r.log" env ECG_LIB=$EL python bench.py --workload lrc-repair \
+                    --forms reference_sequence_per_call,reference_sequence_per_call_threads8 --steps 10 --warmup 2 --no-cpu-baseline
+                done
+              done
+              for f in "$O"/abrepair_*.log; do
+                tail -1 "$f" | python -c "import json,sys; d=json.loads(sys.stdin.read())['results']; print('$f', {k: v['algorithmic_frac'] for k, v in d.items()})"
+              done ;;
     callrate) run call_rate 300 "$O/call_rate.txt" ./tools/call_rate
               run record_cost 300 "$O/record_cost.txt" ./tools/record_cost ;;
     ab) for r in 1 2 3; do
