@@ -211,6 +211,23 @@ def libecg_sha16():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
+def build_provenance():
+    """The libecg.so this run loads, the sources in this tree, and the record __graft_entry__.build() left
+    (lib/build_info.json): whether this .so is the one build() produced from exactly these sources."""
+    out = {"libecg_sha16": libecg_sha16()}
+    try:
+        import __graft_entry__ as G
+        out["sources_sha16"] = G.sources_sha16()
+        info = json.load(open(os.path.join(ROOT, "erasure-codes-prototype_amd", "lib", "build_info.json")))
+        out["build_info"] = info
+        out["built_by_build_from_these_sources"] = (info.get("libecg_sha16") == out["libecg_sha16"] and
+                                                    info.get("sources_sha16") == out["sources_sha16"])
+    except Exception as e:  # noqa: BLE001 -- no record: the line says so
+        out["build_info"] = None
+        out["note"] = f"{type(e).__name__}: {str(e)[:120]}"
+    return out
+
+
 def committed_profile():
     """The committed headline-only rocprofv3 summary (tools/profile_summary.py) and PMC file, named beside
     this run's HIP-event fractions, with whether they were taken on this very libecg.so build."""
@@ -415,6 +432,7 @@ def rs_encode_decode(a, r):
                      "frac_source": "HIP events on this run's stream, averaged over the timed steps",
                      **committed_profile()},
         "parity_checksums": [f"{c:016x}" for c in checks],
+        "build": build_provenance(),
     }
     # every rank's own kernel times and HBM fractions (HIP events on its stream), not rank 0's only
     mine = [enc_avg * 1e3, dec_avg * 1e3, achieved / HBM_PEAK_GBS, dec_bytes / dec_avg / 1e9 / HBM_PEAK_GBS]
@@ -517,6 +535,8 @@ def config3_line(a, r):
                "local_repairs": res["local_repairs"], "global_repairs": res["global_repairs"], "forms": {}}
         for name, v in res["results"].items():
             out["forms"][name] = {**v, **workload_profile(f"config3/{name}")}
+        oks = D.gather_floats([1.0 if all(v["verified"] for v in res["results"].values()) else 0.0], r, device="cuda")
+        out["verified_all_ranks"] = all(x[0] == 1.0 for x in oks)
         del res
         torch.cuda.empty_cache()
         if r.world == 1 and r.rank == 0 and not a.no_cpu_baseline:
@@ -583,6 +603,8 @@ def config4_line(a, r):
                "algorithmic_bytes_per_batch": res["algorithmic_bytes_per_batch"], "forms": {}}
         for name, v in res["results"].items():
             out["forms"][name] = {**v, **workload_profile(f"config4/{name}")}
+        oks = D.gather_floats([1.0 if all(v["verified"] for v in res["results"].values()) else 0.0], r, device="cuda")
+        out["verified_all_ranks"] = all(x[0] == 1.0 for x in oks)
         del res
         torch.cuda.empty_cache()
         if r.world == 1 and r.rank == 0 and not a.no_cpu_baseline:
@@ -626,17 +648,28 @@ def optional_deadline_s() -> float:
 def optional_section(line, r, keys, body):
     """Run body(), which fills line[key] for `keys`, under ecg_dist.deadline: a sub-object that hangs (an
     RCCL exchange across GPUs that never completes, say) must not cost the line the headline measured
-    before it.  On expiry rank 0 prints the line with {"error": ...} for every key not filled yet, and
-    every rank exits 0.  Exceptions inside the sub-objects are caught by the sub-objects themselves."""
+    before it.  On expiry rank 0 prints the line with {"error": ...} for every key not filled yet and
+    "optional_deadline_hit": true, and every rank exits 0 (the line is valid; the field says it was cut).
+    Exceptions inside the sub-objects are caught by the sub-objects themselves.  The watchdog and the main
+    thread settle who finishes the section under one lock: once body() has returned the
+    watchdog does nothing, and once the watchdog has fired the main thread never prints."""
+    import threading
     limit = optional_deadline_s()
+    lock = threading.Lock()
+    state = {"finished": False}
 
     def expire():
+        with lock:
+            if state["finished"]:
+                return  # body() returned first: the main thread prints the full line
+            state["expired"] = True
         try:
             partial = dict(line)
             for key in keys:
                 if key not in partial:
                     partial[key] = {"error": f"not finished within {limit:.0f} s (optional-section deadline, "
                                              "ECG_BENCH_OPTIONAL_DEADLINE_S); the rest of the line stands"}
+            partial["optional_deadline_hit"] = True
             if r.rank == 0:
                 print(json.dumps(partial), flush=True)
         finally:
@@ -644,6 +677,11 @@ def optional_section(line, r, keys, body):
 
     with D.deadline(limit, expire):
         body()
+        with lock:
+            state["finished"] = True
+            expired = state.get("expired", False)
+    if expired:  # the watchdog is printing the line and ending the process: never a second line
+        threading.Event().wait()
 
 
 def config5(a, r, M, k, m):

@@ -165,7 +165,7 @@ int ProgramSet::ensure_ready(hipStream_t st) {
         return ECG_OK;
     }
     if (q != hipErrorNotReady) return ECG_EHIP;
-    if (st != first_stream && hipStreamWaitEvent(st, ready_ev, 0) != hipSuccess) return ECG_EHIP;
+    if (stream_key(st) != first_stream && hipStreamWaitEvent(st, ready_ev, 0) != hipSuccess) return ECG_EHIP;
     return ECG_OK;
 }
 
@@ -236,13 +236,21 @@ void Engine::release_tables(void* p, size_t cls) {
 }
 
 void Engine::retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted) {
+#ifndef ECG_TEST_TSAN_SEEDED_RACE  // test hook: tools/tsan_host.sh seeded must report this unlocked push as a race
     std::lock_guard<std::mutex> lk(rmu_);
+#endif
     for (auto& ps : evicted) retired_.push_back(std::move(ps));
 }
 
-namespace {
-bool never_destroyed(hipStream_t st) { return st == nullptr || st == hipStreamPerThread; }
-}  // namespace
+hipStream_t stream_key(hipStream_t st) {
+#ifdef ECG_TEST_PER_THREAD_SHARED_KEY  // test hook: round 4's one key for every thread's per-thread stream
+    return st;                         // (tools/tsan_host.sh sharedkey must report a device-time hazard)
+#endif
+    if (st != hipStreamPerThread) return st;
+    static std::atomic<uintptr_t> next{1};
+    static thread_local const uintptr_t key = (next.fetch_add(1, std::memory_order_relaxed) << 1) | 1;
+    return (hipStream_t)key;
+}
 
 // One pass over the retired sets (ProgramSet's retirement comment):
 //   1. every unheld set's uncovered stream that may be named now -- `current` (a stream the caller handed
@@ -262,10 +270,12 @@ void Engine::sweep_retired(hipStream_t current, bool has_current) {
     if (over) (void)sync_and_free_unheld();  // the graveyard outgrew ECG_OPT_GRAVEYARD
 }
 
-// A launch on st hit the cover mask: cover the unheld retired sets that wait for st (one event record).
+// A launch on st hit the cover mask: cover the unheld retired sets that wait for st's key (one event record
+// on st, the caller's handle: for hipStreamPerThread, this thread's stream, the one the key names).
 void Engine::cover_retired(hipStream_t st) {
+    const hipStream_t key = stream_key(st);
     std::lock_guard<std::mutex> lk(rmu_);
-    auto it = waiting_.find(st);
+    auto it = waiting_.find(key);
     if (it == waiting_.end()) return;  // another stream with the same mask bit
     std::shared_ptr<ProgramSet::CoverEvent> cover;
     auto& v = it->second;
@@ -287,7 +297,7 @@ void Engine::cover_retired(hipStream_t st) {
             }
             std::lock_guard<std::mutex> sk(ps->smu);
             for (int e = 0; e < ps->nslots; e++)
-                if (ps->slots[e].st == st && !ps->slots[e].cover) ps->slots[e].cover = cover;
+                if (ps->slots[e].st == key && !ps->slots[e].cover) ps->slots[e].cover = cover;
         }
         v[i] = std::move(v.back());
         v.pop_back();
@@ -306,14 +316,17 @@ bool Engine::sweep_locked(hipStream_t current, bool has_current, std::vector<std
         cover_mask_.store(0, std::memory_order_relaxed);
         return false;
     }
-    std::shared_ptr<ProgramSet::CoverEvent> made[3];  // current, null stream, per-thread stream
-    auto cover_for = [&](hipStream_t st) -> std::shared_ptr<ProgramSet::CoverEvent> {
-        const int i = (has_current && st == current) ? 0 : st == nullptr ? 1 : st == hipStreamPerThread ? 2 : -1;
+    // slots hold stream keys: a slot is covered on `current` (the caller's handle, which names the slot's
+    // stream in this thread) when its key is current's, and at once when it is the null stream
+    const hipStream_t cur_key = has_current ? stream_key(current) : nullptr;
+    std::shared_ptr<ProgramSet::CoverEvent> made[2];  // current, null stream
+    auto cover_for = [&](hipStream_t key) -> std::shared_ptr<ProgramSet::CoverEvent> {
+        const int i = (has_current && key == cur_key) ? 0 : key == nullptr ? 1 : -1;
         if (i < 0) return nullptr;
         if (!made[i]) {
             hipEvent_t ev = acquire_event();
             if (!ev) return nullptr;
-            if (hipEventRecord(ev, st) != hipSuccess) {
+            if (hipEventRecord(ev, i == 0 ? current : nullptr) != hipSuccess) {
                 release_event(ev);
                 return nullptr;
             }
@@ -331,7 +344,7 @@ bool Engine::sweep_locked(hipStream_t current, bool has_current, std::vector<std
             std::lock_guard<std::mutex> sk(ps.smu);
             for (int e = 0; e < ps.nslots; e++) {
                 ProgramSet::StreamSlot& sl = ps.slots[e];
-                if (!sl.cover && unheld && (never_destroyed(sl.st) || (has_current && sl.st == current)))
+                if (!sl.cover && unheld && (sl.st == nullptr || (has_current && sl.st == cur_key)))
                     sl.cover = cover_for(sl.st);
                 if (!sl.cover) {
                     if (unheld) waiting_[sl.st].push_back(retired_[i]);
@@ -519,7 +532,7 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
     ps->pinned = acquire_pinned(total, &ps->pinned_class, &e);
     if (!ps->pinned) return fail(e, "hipHostMalloc(program tables)");
     memcpy(ps->pinned, host.data(), total);
-    ps->first_stream = st;
+    ps->first_stream = stream_key(st);
     if ((e = hipMemcpyAsync(ps->mem, ps->pinned, total, hipMemcpyHostToDevice, st)) != hipSuccess) {
         (void)hipStreamSynchronize(st);
         return fail(e, "hipMemcpyAsync(program tables)");
@@ -653,7 +666,7 @@ struct DeferScope {
     int h_up = 0, h_w = 0;
     long long h_B = -1;
     bool h_inplace = false;  // a written block has a region-A slot (read, then written)
-    PtrGroups h_out;         // pending output block addresses (wr = 1), open addressing
+    PtrGroups h_out;         // pending output blocks by B-byte bucket (pending_output_overlaps), open addressing
     size_t h_nout = 0;       // entries in h_out (a block is written at most once per batch: a second write flushes)
     std::unique_ptr<CtxLease> h_ctx;
     ~DeferScope() { release_order_evs(); }
@@ -1510,13 +1523,38 @@ void host_queue_reset() {
     d.h_ctx.reset();  // a context whose batch did not complete drains its streams before its next lessee
 }
 
+// Pending outputs of the deferred host batch, compared by BYTE RANGE (host blocks of one scope
+// may be offsets into one caller buffer).  Every pending output is [p, p + B) with the batch's one block
+// size, and pending outputs are pairwise disjoint (a call touching one flushes first), so a B-byte bucket
+// holds the start of at most one: h_out maps bucket p / B + 1 to wr = 1 and rd = p % B.  A block [a, a + B)
+// overlaps a pending output iff one starts in bucket a / B - 1, a / B or a / B + 1 within B bytes of a.
+void note_pending_output(DeferScope& d, const void* blk, long long B) {
+    if (B <= 0) return;  // an empty block overlaps nothing
+    const uintptr_t p = (uintptr_t)blk, b = (uintptr_t)B;
+    PtrGroups::Slot& s = d.h_out.at((const void*)(p / b + 1));
+    s.wr = 1;
+    s.rd = (int)(p % b);
+}
+
+bool pending_output_overlaps(const DeferScope& d, const void* blk, long long B) {
+    if (B <= 0) return false;
+    const uintptr_t a = (uintptr_t)blk, b = (uintptr_t)B, q = a / b;
+    for (uintptr_t k = q ? q - 1 : 0; k <= q + 1; k++) {
+        const PtrGroups::Slot* s = d.h_out.find_slot((const void*)(k + 1));
+        if (!s || !s->wr) continue;
+        const uintptr_t p = k * b + (uintptr_t)s->rd;
+        if ((p > a ? p - a : a - p) < b) return true;
+    }
+    return false;
+}
+
 }  // namespace
 
 // Record one host-tier call of an open scope with host deferral on.  Returns ECG_OK (recorded), a negative
 // status, or 1: not deferrable (blocks above kStagedMaxBlock, or the call alone overflows the staging) --
-// the caller runs it synchronously after flushing.  A call whose blocks include a pending output of an
-// earlier recorded call, or with another block size or engine, flushes the batch first (blocks are
-// compared by address: blocks of one scope are identical or disjoint).
+// the caller runs it synchronously after flushing.  A call whose blocks overlap a pending output of an
+// earlier recorded call (by byte range, pending_output_overlaps), or with another block size or engine,
+// flushes the batch first.
 int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* blocks, int nblocks, long long B) {
     DeferScope& d = t_defer;
     if (B > (long long)kStagedMaxBlock) return 1;
@@ -1549,7 +1587,7 @@ int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* b
                                    (size_t)(d.h_up + d.h_w + nup + nw) * pitch > kHostDeferMaxBytes);
 #ifndef ECG_TEST_NO_HOST_HAZARD_FLUSH  // test hook: a variant without this flush must fail the random-sequence test
     for (int id = 0; id < nblocks && !flush && d.h_nout; id++)
-        flush = used[id] && d.h_out.last_write(blocks[id]) > 0;
+        flush = used[id] && pending_output_overlaps(d, blocks[id], B);
 #endif
     if (flush)
         if (const int rc = host_flush(); rc != ECG_OK) return rc;
@@ -1583,7 +1621,7 @@ int record_host(Engine* eng, const std::vector<LinearOp>& ops, uint8_t* const* b
         }
         if (written[id]) {
             call.wr.push_back(id);
-            d.h_out.at(blocks[id]).wr = 1;
+            note_pending_output(d, blocks[id], B);
             d.h_nout++;
             d.h_inplace |= upload[id] != 0;
         }
@@ -1831,6 +1869,27 @@ int Engine::run_ptr_batch_multi(const std::vector<const LinearOp*>& ops, const s
         }
         return run_ptr_batch(progs[0], rows, B, st);
     }
+    // One set of matrices is one cache entry, whatever order the calls met them in (per-stripe
+    // decodes of one batch in another order would otherwise build, and retire, a new program set each time).
+    {
+        thread_local std::vector<int> order, rank;
+        order.resize(progs.size());
+        for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+        std::sort(order.begin(), order.end(), [](int a, int b) { return progs[a].coef < progs[b].coef; });
+        rank.resize(progs.size());
+        bool moved = false;
+        for (size_t r = 0; r < order.size(); r++) {
+            rank[order[r]] = (int)r;
+            moved |= order[r] != (int)r;
+        }
+        if (moved) {
+            thread_local std::vector<LinearOp> sorted;
+            sorted.clear();
+            for (int i : order) sorted.push_back(std::move(progs[i]));
+            progs.swap(sorted);
+            for (int& x : pid) x = rank[x];
+        }
+    }
     int status = ECG_OK;
     std::shared_ptr<ProgramSet> ps = program_set(progs, &status, st);
     if (!ps) return status;
@@ -2007,7 +2066,7 @@ namespace {
 // Resident call worker of a device (ECG_OPT_CALL_WORKER > 0; gf_kernels.hpp WorkerArgs).
 // A small synchronous host-tier call normally pays a kernel launch (~4 us of an ~11 us RS(6,4) 1 KiB call);
 // with the worker, a resident kernel polls a descriptor ring in pinned host memory and the call only
-// writes its descriptor (tools/persist_probe.hip: 11.4 -> 4.9 us).  One call at a time goes through it
+// writes its descriptor (profiles/r03/persist/persist_probe.hip: 11.4 -> 4.9 us).  One call at a time goes through it
 // (try_lock): concurrent callers take the launch path, so concurrency is never serialised behind it.
 // The worker runs on a HIGH-PRIORITY stream: HIP maps streams onto a few hardware queues, and a kernel
 // that stays resident on a queue shared with another stream holds that stream's work behind it until it
@@ -2312,7 +2371,7 @@ int Engine::run_host(const std::vector<LinearOp>& ops, uint8_t* const* blocks, i
         }
         // Completion by flags: every workgroup posts a flag once its stores are visible to the host, and the
         // host polls the flags instead of synchronizing the stream -- the runtime's completion round trip is
-        // ~4 us of a ~14 us call (tools/small_call.cpp, profiles/r02/small_call/).  Only for launches whose
+        // ~4 us of a ~14 us call (profiles/r02/small_call/small_call.cpp).  Only for launches whose
         // vector path covers every byte and that fit the flag page; anything else synchronizes as before.
         // the resident call worker, when enabled: one op of at most 16 inputs and 4 outputs, blocks of at
         // most 16 KiB in 4-byte lanes, tables already resident; anything else takes the launch path below
@@ -2445,6 +2504,8 @@ static int row_split(const std::vector<LinearOp>& progs, int S, const void* in_b
     const long long min_k = get_option(ECG_OPT_ROW_SPLIT);
     const int k = progs[0].k_in(), m = progs[0].m_out();
     if (min_k <= 0 || k < min_k || m < 2 || k % m || (long long)S * m > 0x7fffffffLL) return 0;
+    // the disjointness tests below bound spans by their last block, which needs non-negative strides
+    if (iss < 0 || ibs < 0 || oss < 0 || obs < 0) return 0;
     const int kr = k / m;
     int max_src = 0, max_dst = 0;
     for (const LinearOp& op : progs) {

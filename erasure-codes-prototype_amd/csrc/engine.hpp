@@ -38,6 +38,15 @@ constexpr size_t kStagedMaxBytes = 8 << 20;
 
 class Engine;
 
+// A caller stream's identity for comparisons (program-set retirement, upload readiness).  hipStreamPerThread
+// is ONE handle value that names a different stream on every thread, so it is keyed per thread: a serial
+// number unique to the thread for the life of the process, shifted and tagged with bit 0 (real handles are
+// aligned pointers, so no key equals one).  A set noted under such a key is covered only by its own thread --
+// at a launch on hipStreamPerThread, or a cache miss on it -- where the handle names that very stream; a
+// thread that exits leaves its sets to the graveyard (a cover on another thread's per-thread
+// stream could fire while the noting thread's launch was still queued).
+hipStream_t stream_key(hipStream_t st);
+
 struct ProgramSet {
     Engine* owner = nullptr;  // its device memory (one block: tables + ids) goes back to owner's pool
     uint64_t serial = 0;      // unique per set (retirement names sets by it, not by address)
@@ -56,8 +65,9 @@ struct ProgramSet {
     // profiles/r04/stream/).  Instead a launch only notes its stream handle (compared, never passed to
     // HIP).  Once the set is retired and nobody holds it, each noted stream gets a "cover" event recorded on
     // it the next time the library is handed that stream anyway (a later launch or cache miss on it: the
-    // stream is alive then, and a record then follows every earlier launch on it).  The null stream and
-    // hipStreamPerThread are never destroyed, so they are covered at once.  A set whose streams are never
+    // stream is alive then, and a record then follows every earlier launch on it).  The null stream is never
+    // destroyed, so it is covered at once; hipStreamPerThread slots carry their thread's stream_key and are
+    // covered from that thread only.  Slots hold stream_key()s.  A set whose streams are never
     // seen again (destroyed, or idle) waits in a bounded graveyard, emptied by a device synchronize when it
     // outgrows ECG_OPT_GRAVEYARD or on ecg_program_sets_reclaim.  Host-tier launches are not noted: those calls
     // wait for their own completion before they return.  More than kMaxStreams streams -> graveyard.
@@ -72,7 +82,7 @@ struct ProgramSet {
     int nslots = 0;
     bool overflow = false;
     std::atomic<int> nslots_pub{0};  // slots[0, nslots_pub) have their stream set (lock-free launch check)
-    void used_on(hipStream_t st) {  // launch path: note the caller stream
+    void used_on(hipStream_t st) {  // launch path: note the caller stream (its stream_key)
         const int n = nslots_pub.load(std::memory_order_acquire);
         for (int i = 0; i < n; i++)
             if (slots[i].st == st) return;  // the common case: no lock
@@ -88,7 +98,7 @@ struct ProgramSet {
     }
     // upload state (program_set): the tables are copied on the first requesting stream
     hipEvent_t ready_ev = nullptr;
-    hipStream_t first_stream = nullptr;  // compared only
+    hipStream_t first_stream = nullptr;  // stream_key of the uploading stream, compared only
     std::atomic<bool> ready{false};
     void* pinned = nullptr;  // source of the asynchronous upload (pinned pool block, returned once ready)
     size_t pinned_class = 0;
@@ -150,8 +160,9 @@ public:
     // After enqueueing a launch of `ps` on caller stream st (device and batched tiers): note the stream on
     // the set and, if retired sets wait for a cover on a stream hashing like st, cover them on st now.
     void note_launch(ProgramSet& ps, hipStream_t st) {
-        ps.used_on(st);
-        if (cover_mask_.load(std::memory_order_relaxed) & stream_bit(st)) cover_retired(st);
+        const hipStream_t key = stream_key(st);
+        ps.used_on(key);
+        if (cover_mask_.load(std::memory_order_relaxed) & stream_bit(key)) cover_retired(st);
     }
     size_t retired_pending();  // evicted sets not yet freed (sweeps first; no synchronize)
     size_t reclaim();          // synchronize the device, free every retired set nobody holds; pending after
@@ -173,7 +184,7 @@ private:
     // graveyard of sets that cannot be covered outgrows ECG_OPT_GRAVEYARD.
     void retire(std::vector<std::shared_ptr<ProgramSet>>&& evicted);
     void sweep_retired(hipStream_t current, bool has_current);
-    void cover_retired(hipStream_t st);  // a launch on st hit the cover mask
+    void cover_retired(hipStream_t st);  // a launch on st (the caller's handle) hit the cover mask
     // under rmu_: true = the graveyard outgrew ECG_OPT_GRAVEYARD (the caller then runs sync_and_free_unheld)
     bool sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead);
     size_t sync_and_free_unheld();
@@ -202,8 +213,8 @@ private:
     std::unordered_map<std::string, CacheEntry> cache_;  // LRU-bounded by ECG_OPT_PROGRAM_CACHE
     std::mutex rmu_;
     std::vector<std::shared_ptr<ProgramSet>> retired_;
-    // unheld retired sets waiting for a cover on each stream (rebuilt by every sweep; weak: the sets are
-    // owned by retired_), and the stream_bit of every stream in it
+    // unheld retired sets waiting for a cover on each stream key (rebuilt by every sweep; weak: the sets are
+    // owned by retired_), and the stream_bit of every key in it
     std::unordered_map<hipStream_t, std::vector<std::weak_ptr<ProgramSet>>> waiting_;
     std::atomic<uint64_t> cover_mask_{0};
     std::mutex pmu_;
@@ -329,6 +340,7 @@ public:
         count_ = 0;
     }
     int last_write(const void* ptr) const { const Slot* s = find(ptr); return s ? s->wr : 0; }
+    const Slot* find_slot(const void* ptr) const { return find(ptr); }
     int last_touch(const void* ptr) const { const Slot* s = find(ptr); return s ? std::max(s->rd, s->wr) : 0; }
 
 private:

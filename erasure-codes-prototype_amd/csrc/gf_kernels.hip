@@ -837,7 +837,7 @@ int set_option(int opt, long long value) {
     return 0;
 }
 
-// Grid-map auto rule (r01 tools/shape_sweep.py, every k_in x m_out shape): when the outputs are blocks
+// Grid-map auto rule (profiles/r01/shape_sweep.py, every k_in x m_out shape): when the outputs are blocks
 // of the input stripes themselves (encode: [S][k+m][B]), XCD-contiguous chunks (map 1) are 1-3 % faster;
 // when they go to a separate buffer (decode / repair / merge outputs), putting stripe s on XCD s % 8
 // (map 2) is 2-6 % faster.  Pointer-table launches have no single layout and take map 1.

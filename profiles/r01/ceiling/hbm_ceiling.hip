@@ -11,7 +11,7 @@
 //
 // Each lane owns one 16-byte column of a 2 KiB chunk (128-thread workgroups, the engine's shape) or,
 // with IN_FLIGHT > 1, IN_FLIGHT consecutive 2 KiB chunks whose loads are all issued before any use.
-// Build: hipcc -O3 --offload-arch=gfx950 -o hbm_ceiling tools/hbm_ceiling.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o hbm_ceiling profiles/r01/ceiling/hbm_ceiling.hip
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -3,7 +3,7 @@
 0.76 of 8 TB/s while the microbench's decode (after a decode) measures 0.81.  This times the default
 config-2 encode and decode kernels in several orders within one process, HIP events around each.
 
-    python tools/order_probe.py [--reps 6]
+    python profiles/r01/order_probe.py [--reps 6]
 """
 import argparse
 import os

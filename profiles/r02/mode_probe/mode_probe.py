@@ -8,7 +8,7 @@ The per-stripe calls are recorded in pair-swapped stripe order (1, 0, 3, 2, ...)
 nearly the same DRAM order, but not one strided batch, so the flush takes the pointer-table launch.
 --cols runs the PTRS launch at several ECG_OPT_COLS_PER_WG values (16-byte columns per workgroup).
 
-    python tools/mode_probe.py [--block 1048576] [--stripes 4096] [--reps 5] [--cols 0,256,512]
+    python profiles/r02/mode_probe/mode_probe.py [--block 1048576] [--stripes 4096] [--reps 5] [--cols 0,256,512]
 """
 import argparse
 import os

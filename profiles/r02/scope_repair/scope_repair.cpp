@@ -9,9 +9,9 @@
 //            single-launch form the scratch composition should match).
 // Azure-LRC(12,2,2), local repairs (block e = local[s mod 14] of stripe s), S stripes of 16 blocks.
 // Every form is checked against the lost blocks.  Prints one JSON line per form.
-// Build: hipcc -O2 -std=c++20 --offload-arch=gfx950 -Iinclude tools/scope_repair.cpp -Lerasure-codes-prototype_amd/lib
-//        -lecg -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o tools/scope_repair
-// Run:   tools/scope_repair [B_bytes] [S] [steps] [chunk_stripes]
+// Build: hipcc -O2 -std=c++20 --offload-arch=gfx950 -Iinclude profiles/r02/scope_repair/scope_repair.cpp -Lerasure-codes-prototype_amd/lib
+//        -lecg -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o profiles/r02/scope_repair/scope_repair
+// Run:   profiles/r02/scope_repair/scope_repair [B_bytes] [S] [steps] [chunk_stripes]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

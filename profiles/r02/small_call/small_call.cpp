@@ -17,8 +17,8 @@
 //   callD / call16, decD / dec16   the product's encode / decode with the latency kernel at 4 bytes
 //            per lane (ECG_OPT_LAT_DWORD_BYTES default) and at 16 bytes per lane (option 0), alternated
 // Run under rocprofv3 --kernel-trace --hip-trace --stats to split each into API and kernel time.
-// Build: hipcc -O2 -std=c++20 --offload-arch=gfx950 -Iinclude tools/small_call.cpp -Lerasure-codes-prototype_amd/lib -lecg
-//        -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o tools/small_call
+// Build: hipcc -O2 -std=c++20 --offload-arch=gfx950 -Iinclude profiles/r02/small_call/small_call.cpp -Lerasure-codes-prototype_amd/lib -lecg
+//        -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o profiles/r02/small_call/small_call
 #include <hip/hip_runtime.h>
 
 #include <chrono>

@@ -2,7 +2,7 @@
 // descriptors AND small-call input data from HBM instead of reading them over PCIe (one round trip each).
 // Tries hipExtMallocWithFlags(fine-grained / uncached) and the HSA pool API with CPU access granted;
 // reports the pointer attributes, checks CPU writes against a device read, and times CPU writes of 6 KiB.
-// Build: hipcc -O2 -std=c++17 --offload-arch=gfx950 tools/bar_probe.hip -lhsa-runtime64 -o tools/bar_probe
+// Build: hipcc -O2 -std=c++17 --offload-arch=gfx950 profiles/r03/persist/bar_probe.hip -lhsa-runtime64 -o profiles/r03/persist/bar_probe
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>

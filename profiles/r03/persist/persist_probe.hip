@@ -19,9 +19,9 @@
 // minus the launch.  Device tier (asynchronous, HBM blocks): descriptors carry HBM pointers and are posted
 // back to back; the host only waits for a ring slot's previous call before reusing it.
 //
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Iinclude -Ierasure-codes-prototype_amd/csrc tools/persist_probe.hip
-//        -Lerasure-codes-prototype_amd/lib -lecg -lhsa-runtime64 -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o tools/persist_probe
-// Run:   timeout -k 10 120 tools/persist_probe [calls]
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Iinclude -Ierasure-codes-prototype_amd/csrc profiles/r03/persist/persist_probe.hip
+//        -Lerasure-codes-prototype_amd/lib -lecg -lhsa-runtime64 -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o profiles/r03/persist/persist_probe
+// Run:   timeout -k 10 120 profiles/r03/persist/persist_probe [calls]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -2,7 +2,7 @@
 // GPU timeline when its work is tiny, as a function of the kernel-argument size.  The device tier's
 // per-call path (one ErasureCode call per stripe on HBM blocks) is one such launch per call, with a
 // ~1.4 KiB GfLaunch argument block (160 inline block pointers).
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/launch_floor.hip -o tools/launch_floor
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 profiles/r04/lat_tables/launch_floor.hip -o profiles/r04/lat_tables/launch_floor
 #include <hip/hip_runtime.h>
 
 #include <chrono>

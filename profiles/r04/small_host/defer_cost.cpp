@@ -2,8 +2,8 @@
 // one jerasure_matrix_encode per RS(6,4) stripe on host buffers -- inside a batch scope with host deferral
 // (ecg_batch_defer_host).  Reports the host time per recorded call and the time of the flush at
 // ecg_batch_end (one H2D, the grouped launches, one D2H, the scatter into the caller's buffers).
-// Build: hipcc -O2 -std=c++17 --offload-arch=gfx950 -Iinclude tools/defer_cost.cpp -Lerasure-codes-prototype_amd/lib -lecg
-//        -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o tools/defer_cost
+// Build: hipcc -O2 -std=c++17 --offload-arch=gfx950 -Iinclude profiles/r04/small_host/defer_cost.cpp -Lerasure-codes-prototype_amd/lib -lecg
+//        -Wl,-rpath,'$ORIGIN/../erasure-codes-prototype_amd/lib' -o profiles/r04/small_host/defer_cost
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>

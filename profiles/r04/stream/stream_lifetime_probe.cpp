@@ -1,4 +1,4 @@
-// Build: hipcc -O1 -g -std=c++17 --offload-arch=gfx950 tools/stream_lifetime_probe.cpp -o tools/stream_lifetime_probe
+// Build: hipcc -O1 -g -std=c++17 --offload-arch=gfx950 profiles/r04/stream/stream_lifetime_probe.cpp -o profiles/r04/stream/stream_lifetime_probe
 // What the HIP runtime does with a stream handle or an event after hipStreamDestroy:
 // one case per process (a case may crash; the runner starts each under its own timeout).
 //   1 query_after_destroy   event recorded on S (work queued), S destroyed, then query / sync the event

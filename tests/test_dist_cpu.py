@@ -293,6 +293,7 @@ def test_bench_optional_section_deadline_keeps_the_line():
     assert len(lines) == 1, p.stdout
     assert lines[0]["n_gpus"] == 2 and len(lines[0]["ranks"]) == 2
     assert "deadline" in lines[0]["optional"]["error"]
+    assert lines[0].get("optional_deadline_hit") is True
     # without the stall the same section completes
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
                         "--timeout", "200"], capture_output=True, text=True, timeout=300, cwd=ROOT,
@@ -300,6 +301,7 @@ def test_bench_optional_section_deadline_keeps_the_line():
     assert p.returncode == 0, p.stderr[-2000:]
     (line,) = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert line["optional"] == {"ok": True}
+    assert "optional_deadline_hit" not in line
 
 
 def test_deadline_disarms_and_fires():

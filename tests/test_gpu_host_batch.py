@@ -200,3 +200,32 @@ def test_deferred_host_random_sequences_match_sequential(ecg, oracle, torch_cuda
     for B in sizes:
         for j, (a, r) in enumerate(zip(pools[B], ref[B])):
             assert np.array_equal(a, r), (seed, B, j)
+
+
+@pytest.mark.parametrize("shift", [1, 16, 500, 1023])
+def test_deferred_host_partially_overlapping_blocks(ecg, oracle, torch_cuda, shift):
+    """blocks of one scope need not be identical-or-disjoint.  Call 1 writes its parities into a
+    caller buffer; call 2 reads a block that starts `shift` bytes into call 1's first parity (an offset view
+    of the same buffer).  Call 2 must read call 1's output, not the bytes staged before it: the pending
+    outputs are compared by byte range, so call 2 flushes the batch first.  Both against the oracle run
+    call by call."""
+    k, m, B = 6, 4, 1024
+    rng = np.random.default_rng(shift)
+    M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
+    data1 = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(k)]
+    region = rng.integers(0, 256, (m + 1) * B, dtype=np.uint8)  # call 1's parities live in region[0:m*B]
+    out1 = [region[i * B:(i + 1) * B] for i in range(m)]
+    data2 = [region[shift:shift + B]] + [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(k - 1)]
+    out2 = [np.zeros(B, np.uint8) for _ in range(m)]
+    # the oracle, call by call on copies of the same buffers
+    r_region = region.copy()
+    r_out1 = [r_region[i * B:(i + 1) * B] for i in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, data1, r_out1, B)
+    r_data2 = [r_region[shift:shift + B].copy()] + [d.copy() for d in data2[1:]]
+    r_out2 = [np.zeros(B, np.uint8) for _ in range(m)]
+    oracle.jerasure_matrix_encode(k, m, M, r_data2, r_out2, B)
+    with ecg.batch(host=True):
+        assert ecg.jerasure_matrix_encode(k, m, M, data1, out1, B) == 0
+        assert ecg.jerasure_matrix_encode(k, m, M, data2, out2, B) == 0
+    assert np.array_equal(region, r_region)
+    assert all(np.array_equal(a, b) for a, b in zip(out2, r_out2))

@@ -314,6 +314,84 @@ def test_eviction_retires_across_destroyed_and_reused_streams(ecg, oracle):
         ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
 
 
+def test_per_thread_stream_sets_are_covered_only_by_their_thread(ecg, oracle):
+    """hipStreamPerThread is one handle value naming a different stream on every thread.
+    Thread A builds program set P_A (one call, synchronized), queues ~90 ms of encodes on ITS per-thread
+    stream, then calls P_A again; that launch, noted under the handle, waits behind the queue.  Thread B, on ITS per-thread stream, forces
+    P_A's eviction (cache of 2) with twenty new programs of the same shape, synchronizing its own stream
+    after each.  A cover recorded on B's stream would fire at once, P_A's tables would return to the pool,
+    and B's next upload would overwrite them while A's call is still queued.  A's result must equal the
+    oracle's; the library may cover P_A only from thread A (engine.hpp stream_key).  On the GPU this
+    discriminates only when the two per-thread streams land on different hardware queues; the CPU harness
+    (tools/tsan_host.sh sharedkey, tests/test_sanitize.py) checks the same scenario deterministically."""
+    import threading
+
+    import torch
+    hip = _hip()
+    PER_THREAD = 2  # hipStreamPerThread
+    saved = ecg.get_option(ecg.ECG_OPT_PROGRAM_CACHE)
+    rng = np.random.default_rng(23)
+    Bs = 64 << 10
+    blocks = torch.from_numpy(rng.integers(0, 256, (4, Bs), dtype=np.uint8)).cuda()
+    host = blocks.cpu().numpy()
+    mat_a = [int(x) for x in rng.integers(2, 256, 4 * 2)]
+    mats_b = [[int(x) for x in rng.integers(2, 256, 4 * 2)] for _ in range(20)]
+    out_a = torch.zeros((2, Bs), dtype=torch.uint8, device="cuda")
+    outs_b = [torch.zeros((2, Bs), dtype=torch.uint8, device="cuda") for _ in mats_b]
+    big = torch.empty((64, 14, 1 << 20), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(big, 0x7EED)
+    M = ecg.reed_sol_vandermonde_coding_matrix(10, 4)
+    torch.cuda.synchronize()
+    queued, b_done, errors = threading.Event(), threading.Event(), []
+
+    def thread_a():
+        try:
+            # P_A built and uploaded first, so nothing but the queued launch below holds its tables
+            ecg.dev_matrix_encode(4, 2, mat_a, [blocks[j] for j in range(4)], [out_a[0], out_a[1]], Bs,
+                                  stream=PER_THREAD)
+            assert hip.hipStreamSynchronize(PER_THREAD) == 0
+            out_a.zero_()
+            torch.cuda.synchronize()
+            for _ in range(600):  # ~90 ms of work ahead of the call below, on A's per-thread stream
+                ecg.encode_batch(10, 4, M, big[:, :10], big[:, 10:], stream=PER_THREAD)
+            ecg.dev_matrix_encode(4, 2, mat_a, [blocks[j] for j in range(4)], [out_a[0], out_a[1]], Bs,
+                                  stream=PER_THREAD)
+            queued.set()
+            b_done.wait(60)
+            assert hip.hipStreamSynchronize(PER_THREAD) == 0
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+            queued.set()
+
+    def thread_b():
+        try:
+            queued.wait(60)
+            for Mi, out in zip(mats_b, outs_b):
+                ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs, stream=PER_THREAD)
+                assert hip.hipStreamSynchronize(PER_THREAD) == 0
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+        finally:
+            b_done.set()
+
+    try:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, 2)
+        ta, tb = threading.Thread(target=thread_a), threading.Thread(target=thread_b)
+        ta.start()
+        tb.start()
+        ta.join(120)
+        tb.join(120)
+        assert not errors, errors
+        torch.cuda.synchronize()
+        for Mi, out in [(mat_a, out_a)] + list(zip(mats_b, outs_b)):
+            want = [np.zeros(Bs, np.uint8) for _ in range(2)]
+            oracle.jerasure_matrix_encode(4, 2, Mi, [host[j] for j in range(4)], want, Bs)
+            assert np.array_equal(out.cpu().numpy(), np.stack(want)), "a call on hipStreamPerThread read reused tables"
+        assert ecg.lib().ecg_program_sets_reclaim() == 0
+    finally:
+        ecg.set_option(ecg.ECG_OPT_PROGRAM_CACHE, saved)
+
+
 def test_graveyard_bound_frees_sets_of_streams_never_seen_again(ecg, oracle):
     """Evicted sets whose streams the library is never handed again cannot be covered (engine.hpp
     ProgramSet): they wait in the graveyard, which one device synchronize empties once it outgrows
