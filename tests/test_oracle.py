@@ -214,6 +214,26 @@ def test_simd_baseline_matches_scalar(oracle):
             assert (out[(s * m + i) * B:(s * m + i + 1) * B] == a[i]).all()
 
 
+
+def test_call_sequence_baseline_matches_call_by_call(oracle):
+    """bench.py's config3 / config4 CPU baselines (ref.call_seq_batch_mt): a per-stripe sequence of
+    jerasure_matrix_encode(kin, 1) calls through scratch blocks, several threads, equals the same calls made
+    one by one -- here a partial-decoding repair (two partials + perform_addition) and a GENERAL row."""
+    S, nb, B = 9, 8, 1000 + 13
+    stripes = oracle.splitmix_bytes(7, 0, S * nb * B).reshape(S, nb, B)
+    out = np.zeros((S, 2, B), np.uint8)
+    pats = [[(nb + 2, [0, 1, 2], [1, 1, 1]), (nb + 3, [3, 4, 5], [7, 1, 9]), (nb, [nb + 2, nb + 3], [1, 1])],
+            [(nb + 1, [6, 7, 0], [3, 200, 1]), (nb, [nb + 1], [1])]]
+    pat = np.arange(S) % 2
+    assert oracle.call_seq_batch_mt(stripes, out, pats, pat, 2, 4) > 0
+    for s in range(S):
+        blocks = [stripes[s, j].copy() for j in range(nb)] + [np.zeros(B, np.uint8) for _ in range(4)]
+        for dst, src, coef in pats[pat[s]]:
+            res = [np.zeros(B, np.uint8)]
+            oracle.jerasure_matrix_encode(len(src), 1, coef, [blocks[i] for i in src], res, B)
+            blocks[dst] = res[0]
+        assert np.array_equal(out[s, 0], blocks[nb]), s
+
 # ------------------------------------------------------------- reference property tests, made live
 
 def _stripe(ec, B, seed):
