@@ -15,7 +15,8 @@
 //   hipcc -O2 -std=c++17 -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -Ierasure-codes-prototype_amd/csrc \
 //     -c tools/movement_ceiling.cpp -o /tmp/mc.o
 //   hipcc --offload-arch=gfx950 /tmp/mc.o erasure-codes-prototype_amd/build/gf_kernels.o -o tools/movement_ceiling
-// Run: tools/movement_ceiling [rounds=3] [reps=10] [stripes=4096]
+// Run: tools/movement_ceiling [rounds=3] [reps=10] [stripes=4096] [case-name filter]
+// Knobs of the launch (read by the library at first use): ECG_GRID_MAP, ECG_MAP_GROUP, ECG_COLS_PER_WG, ECG_NT.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -61,6 +62,7 @@ int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 3;
     const int reps = argc > 2 ? atoi(argv[2]) : 10;
     const int S = argc > 3 ? atoi(argv[3]) : 4096;
+    const std::string only = argc > 4 ? argv[4] : "";  // run only the cases whose name contains this
     const long long B = 1LL << 20;
     const int n = 14;
     const size_t stripe_bytes = (size_t)n * B;
@@ -76,6 +78,10 @@ int main(int argc, char** argv) {
                                {"dec_general 10->1", 10, 1, false, 1, true},
                                {"dec_zero    10->1", 10, 1, true, 0, true},
                                {"copy_zero    1->1", 1, 1, true, 0, true}};
+    if (!only.empty())
+        cases.erase(std::remove_if(cases.begin(), cases.end(),
+                                   [&](const Case& c) { return c.name.find(only) == std::string::npos; }),
+                    cases.end());
     for (Case& c : cases) {
         std::vector<CoefTab> tabs((size_t)c.k * c.m);
         for (int j = 0; j < c.k; j++)
