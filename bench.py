@@ -501,7 +501,13 @@ def seq_cpu_baseline(nb, nout, B, patterns, pat_of, target_s, nscr, S, fill=None
     from oracle import ref
     ref.build()
     threads, facts = host_cpus()
-    stripes = ref.splitmix_bytes(0xEC0DE, 0, S * nb * B).reshape(S, nb, B)
+    # one stripe of splitmix bytes, the others derived from it by a per-stripe byte (distinct blocks at the
+    # cost of one XOR pass: the sample runs to GiBs, and generating it must not outlast the timing)
+    base = ref.splitmix_bytes(0xEC0DE, 0, nb * B).reshape(1, nb, B)
+    stripes = np.empty((S, nb, B), np.uint8)
+    for i in range(S):
+        np.bitwise_xor(base[0], np.uint8((37 * i + 11) & 0xFF), out=stripes[i])
+    del base
     if fill is not None:
         fill(stripes)
     out = np.zeros((S, nout, B), np.uint8)
@@ -625,7 +631,7 @@ def config4_cpu_baseline(a):
     calls = [(nb + row, [half * 25 + bid(row, col) for half in range(2) for col in range(4)], [1] * 8)
              for row in range(5)]
     threads, _ = host_cpus()
-    S = 2 * threads
+    S = threads  # 200 MiB per merge: 3.2 GiB of host memory at 16 threads
     t, reps, threads, facts, blocks, out = seq_cpu_baseline(nb, 5, B, [calls], None, a.cpu_seconds / 4, 0, S)
     ok = True
     for row, (_, src, _) in enumerate(calls):

@@ -349,3 +349,18 @@ def test_dist_init_passes_timeout(monkeypatch):
     D.init(D.Rank(0, 2, 0), "nccl", device="cuda:0")
     assert seen == {"backend": "nccl", "timeout": datetime.timedelta(seconds=42), "device_id": "cuda:0"}
     D.init(D.Rank(0, 1, 0), "gloo")  # one rank: no process group at all
+
+
+def test_bench_config34_cpu_baselines_verify():
+    """bench.py's config3 / config4 CPU baselines (the oracle's run of the same per-stripe calls, reported
+    beside the GPU forms) repair every sampled block correctly and report a rate; CPU only."""
+    import types
+
+    sys.path.insert(0, ROOT)
+    import bench
+    a = types.SimpleNamespace(cpu_seconds=0.4)
+    c3 = bench.config3_cpu_baseline(a)
+    assert c3["verified"] is True and c3["value"] > 0 and c3["repairs_per_s"] > 0, c3
+    assert c3["kind"] == "port" and c3["cores"] >= 1
+    c4 = bench.config4_cpu_baseline(a)
+    assert c4["verified"] is True and c4["value"] > 0 and c4["merges_per_s"] > 0, c4
