@@ -37,6 +37,7 @@ int* orc_reed_sol_vandermonde_coding_matrix(int k, int m);
 void orc_free(void* p);
 void hip_stub_stall(hipStream_t st, int ms);  // tests/tsan/hip_stub.cpp test hooks
 long hip_stub_hazards();
+long hip_stub_not_ready();
 }
 
 namespace {
@@ -44,6 +45,7 @@ namespace {
 std::atomic<int> g_fail{0};
 std::atomic<long> g_checks{0};
 std::atomic<const char*> g_doing[64];  // what each thread is doing (the watchdog prints it)
+std::atomic<int> g_max_retiring{0};    // the most evicted program sets seen waiting for retirement at once
 
 #define CHECK(cond, ...)                                  \
     do {                                                  \
@@ -343,7 +345,12 @@ struct Worker {
                     doing = "reclaim / options";
                     if (pick(2)) ecg_program_sets_reclaim();
                     else ecg_set_option(ECG_OPT_PROGRAM_CACHE, 4 + 2 * pick(2));
-                    (void)ecg_program_sets_retiring();
+                    {
+                        const int r = ecg_program_sets_retiring();
+                        int seen = g_max_retiring.load();
+                        while (r > seen && !g_max_retiring.compare_exchange_weak(seen, r)) {
+                        }
+                    }
                     (void)ecg_program_cache_size();
                     break;
             }
@@ -465,7 +472,12 @@ int main(int argc, char** argv) {
     }
     ecg_set_device(0);
     const long hazards = hip_stub_hazards();
+    // the run must have exercised the asynchronous paths it is for: queries that found work still pending,
+    // and evicted sets waiting for their covers
+    printf("coverage: %ld not-ready queries, up to %d evicted sets waiting at once\n", hip_stub_not_ready(),
+           g_max_retiring.load());
+    const bool covered = hip_stub_not_ready() > 0 && g_max_retiring.load() > 0;
     printf("engine race done: %d threads x %d ops, %ld checks, %d failed, %ld device-time hazards, %d sets left after "
-           "reclaim\n", T, ops, g_checks.load(), g_fail.load(), hazards, left);
-    return g_fail.load() == 0 && hazards == 0 && left == 0 ? 0 : 1;
+           "reclaim%s\n", T, ops, g_checks.load(), g_fail.load(), hazards, left, covered ? "" : ", PATHS NOT EXERCISED");
+    return g_fail.load() == 0 && hazards == 0 && left == 0 && covered ? 0 : 1;
 }

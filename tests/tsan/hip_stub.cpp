@@ -74,6 +74,7 @@ struct State {
     };
     std::vector<Reader> readers;
     std::atomic<long> hazards{0};
+    std::atomic<long> not_ready{0};  // event / stream queries answered hipErrorNotReady (asynchrony exercised)
 };
 State& S() {
     static State* s = [] {  // never destroyed: threads may still call in during exit
@@ -397,6 +398,7 @@ extern "C" void hip_stub_stall(hipStream_t st, int ms) {  // work worth `ms` of 
     s->done = next_start(s) + std::chrono::milliseconds(ms);
 }
 extern "C" long hip_stub_hazards() { return S().hazards.load(); }
+extern "C" long hip_stub_not_ready() { return S().not_ready.load(); }
 
 hipError_t hipMalloc(void** p, size_t n) {
     *p = alloc(n, hipMemoryTypeDevice);
@@ -478,7 +480,9 @@ hipError_t hipStreamDestroy(hipStream_t st) {
 }
 hipError_t hipStreamQuery(hipStream_t st) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
-    return clk::now() >= as_stream(st)->done ? hipSuccess : hipErrorNotReady;
+    if (clk::now() >= as_stream(st)->done) return hipSuccess;
+    S().not_ready++;
+    return hipErrorNotReady;
 }
 hipError_t hipStreamSynchronize(hipStream_t st) {
     clk::time_point t;
@@ -535,7 +539,9 @@ hipError_t hipEventRecord(hipEvent_t ev, hipStream_t st) {
 hipError_t hipEventQuery(hipEvent_t ev) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     const Event* e = reinterpret_cast<const Event*>(ev);
-    return (!e->recorded || clk::now() >= e->done) ? hipSuccess : hipErrorNotReady;
+    if (!e->recorded || clk::now() >= e->done) return hipSuccess;
+    S().not_ready++;
+    return hipErrorNotReady;
 }
 hipError_t hipEventSynchronize(hipEvent_t ev) {
     clk::time_point t;

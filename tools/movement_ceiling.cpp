@@ -15,7 +15,8 @@
 //   hipcc -O2 -std=c++17 -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -Ierasure-codes-prototype_amd/csrc \
 //     -c tools/movement_ceiling.cpp -o /tmp/mc.o
 //   hipcc --offload-arch=gfx950 /tmp/mc.o erasure-codes-prototype_amd/build/gf_kernels.o -o tools/movement_ceiling
-// Run: tools/movement_ceiling [rounds=3] [reps=10] [stripes=4096] [case-name filter]
+// Run: tools/movement_ceiling [rounds=3] [reps=10] [stripes=4096] [case-name filter] [maps]
+//   maps: the first selected case under grid maps 1 / 2 (G = 1, 16, 64, 128) / 0, interleaved round by round
 // Knobs of the launch (read by the library at first use): ECG_GRID_MAP, ECG_MAP_GROUP, ECG_COLS_PER_WG, ECG_NT.
 #include <hip/hip_runtime.h>
 
@@ -126,6 +127,45 @@ int main(int argc, char** argv) {
     for (auto& e : ev) CK(hipEventCreate(&e));
     printf("S=%d B=%lld grid_map option=%lld nt=%lld (fraction of 8 TB/s, algorithmic bytes / HIP-event time)\n", S, B,
            ecg::get_option(ECG_OPT_GRID_MAP), ecg::get_option(ECG_OPT_NT));
+    // "maps" mode: the first case under each grid-map setting in turn, interleaved round by round in this one
+    // process (the settings are library options), so placement and clock drift hit every setting alike
+    if (argc > 5 && std::string(argv[5]) == "maps") {
+        struct Setting {
+            const char* name;
+            long long map, group;
+            std::vector<double> ms;
+        };
+        std::vector<Setting> st = {{"map1 (XCD-contiguous)", 1, 1, {}}, {"map2 G=1", 2, 1, {}}, {"map2 G=16", 2, 16, {}},
+                                   {"map2 G=64", 2, 64, {}}, {"map2 G=128", 2, 128, {}}, {"map0 (linear)", 0, 1, {}}};
+        Case& c = cases.at(0);
+        for (int r = 0; r < rounds; r++)
+            for (Setting& x : st) {
+                ecg::set_option(ECG_OPT_GRID_MAP, x.map);
+                ecg::set_option(ECG_OPT_MAP_GROUP, x.group);
+                for (int w = 0; w < 2; w++) launch(c);
+                CK(hipEventRecord(ev[0], nullptr));
+                for (int i = 0; i < reps; i++) {
+                    launch(c);
+                    CK(hipEventRecord(ev[i + 1], nullptr));
+                }
+                CK(hipEventSynchronize(ev[reps]));
+                for (int i = 0; i < reps; i++) {
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+                    x.ms.push_back(ms);
+                }
+            }
+        const double bytes = (double)S * (c.k + c.m) * B;
+        for (Setting& x : st) {
+            std::sort(x.ms.begin(), x.ms.end());
+            double avg = 0;
+            for (double v : x.ms) avg += v;
+            avg /= x.ms.size();
+            printf("%s | %-22s avg %.4f ms  median %.4f  | frac avg %.4f  median %.4f\n", c.name.c_str(), x.name, avg,
+                   x.ms[x.ms.size() / 2], bytes / (avg * 1e-3) / 8e12, bytes / (x.ms[x.ms.size() / 2] * 1e-3) / 8e12);
+        }
+        return 0;
+    }
     for (int r = 0; r < rounds; r++) {
         for (Case& c : cases) {
             for (int w = 0; w < 2; w++) launch(c);
