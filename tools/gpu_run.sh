@@ -31,8 +31,12 @@ cd "$GRAFT_REPO_ROOT"
 R=$GRAFT_REPO_ROOT
 O=gpurun_out/${OUT:-run}
 mkdir -p "$O"
+# heartbeat under gpurun_out/ (steps such as the PMC passes print nothing for minutes)
+( while sleep 30; do date +%T >> "$O/heartbeat"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 PYT="python -u -m pytest -p no:cacheprovider --timeout 120 --timeout-method thread"
-HEADLINE="--no-config5 --no-ring --no-host-path"
+HEADLINE="--no-config5 --no-ring --no-host-path --no-configs34"
 
 run() {  # name limit log cmd...  (the command's output goes to log; the status line to this script's stdout)
   local name=$1 lim=$2 log=$3; shift 3
@@ -75,6 +79,7 @@ for step in "$@"; do
     headline) run headline 400 "$O/bench_headline.log" python bench.py --no-cpu-baseline $HEADLINE
            tail -1 "$O/bench_headline.log" | cut -c1-400 ;;
     prof) prof prof prof.log --steps 40 --warmup 3 --no-cpu-baseline
+          rm -f "$O/prof/run_kernel_trace.csv"  # 10^5 rows (config 3's per-call forms): the stats stay
           prof prof_headline prof_headline.log --steps 40 --warmup 3 --no-cpu-baseline $HEADLINE ;;
     pmc) pmc FETCH_SIZE fetch; pmc WRITE_SIZE write
          python tools/parse_pmc.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" \
@@ -107,7 +112,9 @@ for step in "$@"; do
                spec="$spec config4/$f=$O/w34/c4_$f/run_kernel_trace.csv:$O/w34_c4_$f.log:$f"
              done
              python tools/workload_profile.py "$O/workload_profile.json" $spec > "$O/workload_profile.log" 2>&1 \
-               && echo "workload_profile ok" || exit 1 ;;
+               && echo "workload_profile ok" || exit 1
+             # the per-call forms' traces run to 10^5 rows each: summarised above, the kernel stats stay
+             rm -f "$O"/w34/*/run_kernel_trace.csv ;;
     ceiling) run ceiling 200 "$O/ceiling.txt" ./tools/movement_ceiling 4 10
              (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$O/ceiling_prof" -o run \
                 --output-format csv -- "$R/tools/movement_ceiling" 2 10 > "$R/$O/ceiling_prof.txt" 2>&1)

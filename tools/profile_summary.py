@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Headline profile summary read by bench.py's roofline object -> profiles/headline_profile.json.
 
-Inputs: the rocprofv3 --kernel-trace CSV of `bench.py --no-config5 --no-ring --no-host-path` (the headline
+Inputs: the rocprofv3 --kernel-trace CSV of `bench.py --no-config5 --no-ring --no-host-path --no-configs34` (the headline
 alone, so the encode / decode instantiations run nothing else) and the PMC traffic JSON of the same tree
 (tools/parse_pmc.py).  Output: per-kernel average and median launch durations over every launch in the
 trace, the fractions of 8 TB/s they give for the algorithmic bytes, the PMC bytes, and the sha256 prefixes

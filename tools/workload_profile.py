@@ -56,7 +56,9 @@ def summarise(trace, log, form):
     busy = sum(sum(v) for v in per.values())
     dom = max(per, key=lambda k: sum(per[k]))
     d = per[dom]
-    return {"source": os.path.relpath(trace, ROOT), "bench_log": os.path.relpath(log, ROOT), "batches": batches,
+    stats = os.path.join(os.path.dirname(trace), "run_kernel_stats.csv")
+    return {"source": os.path.relpath(trace, ROOT) + " (summarised on the box; the trace is not kept)",
+            "kernel_stats": os.path.relpath(stats, ROOT), "bench_log": os.path.relpath(log, ROOT), "batches": batches,
             "algorithmic_bytes_per_batch": alg,
             "kernels": {k: {"launches": len(v), "avg_us": round(sum(v) / len(v) / 1e3, 3),
                             "min_us": round(min(v) / 1e3, 3), "total_ms": round(sum(v) / 1e6, 3)}
