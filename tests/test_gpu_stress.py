@@ -235,6 +235,7 @@ def _hip():
     h.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
     h.hipStreamDestroy.argtypes = [ctypes.c_void_p]
     h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    h.hipStreamQuery.argtypes = [ctypes.c_void_p]
     return h
 
 
@@ -343,9 +344,15 @@ def test_per_thread_stream_sets_are_covered_only_by_their_thread(ecg, oracle):
     M = ecg.reed_sol_vandermonde_coding_matrix(10, 4)
     torch.cuda.synchronize()
     queued, b_done, errors = threading.Event(), threading.Event(), []
+    a_made, b_made, still_queued = threading.Event(), threading.Event(), []
 
     def thread_a():
         try:
+            # the two per-thread streams are created back to back, so the runtime deals them to different
+            # hardware queues (it hands new streams the queues in turn) and B's work does not wait behind A's
+            assert hip.hipStreamQuery(PER_THREAD) == 0
+            a_made.set()
+            b_made.wait(60)
             # P_A built and uploaded first, so nothing but the queued launch below holds its tables
             ecg.dev_matrix_encode(4, 2, mat_a, [blocks[j] for j in range(4)], [out_a[0], out_a[1]], Bs,
                                   stream=PER_THREAD)
@@ -358,6 +365,7 @@ def test_per_thread_stream_sets_are_covered_only_by_their_thread(ecg, oracle):
                                   stream=PER_THREAD)
             queued.set()
             b_done.wait(60)
+            still_queued.append(hip.hipStreamQuery(PER_THREAD) != 0)  # A's call not yet run when B finished
             assert hip.hipStreamSynchronize(PER_THREAD) == 0
         except Exception as e:  # noqa: BLE001
             errors.append(e)
@@ -365,6 +373,9 @@ def test_per_thread_stream_sets_are_covered_only_by_their_thread(ecg, oracle):
 
     def thread_b():
         try:
+            a_made.wait(60)
+            assert hip.hipStreamQuery(PER_THREAD) == 0
+            b_made.set()
             queued.wait(60)
             for Mi, out in zip(mats_b, outs_b):
                 ecg.dev_matrix_encode(4, 2, Mi, [blocks[j] for j in range(4)], [out[0], out[1]], Bs, stream=PER_THREAD)
@@ -382,6 +393,8 @@ def test_per_thread_stream_sets_are_covered_only_by_their_thread(ecg, oracle):
         ta.join(120)
         tb.join(120)
         assert not errors, errors
+        # whether the scenario could discriminate on this box: B's evictions ran while A's call was queued
+        print(f"A's call still queued when B finished: {still_queued}")
         torch.cuda.synchronize()
         for Mi, out in [(mat_a, out_a)] + list(zip(mats_b, outs_b)):
             want = [np.zeros(Bs, np.uint8) for _ in range(2)]
