@@ -12,7 +12,7 @@
 // Policies 2-4 are vector stores written with inline asm (global_store_dwordx4 with cache-policy bits).
 // Every variant's parities are checked on the host for a few stripes; fractions = (10 + 4) * B * S / time / 8 TB/s,
 // HIP events, variants interleaved round by round.
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/store_policy_probe.hip -o tools/store_policy_probe
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 profiles/r05/sweep/store_policy_probe.hip -o tools/store_policy_probe
 // Run:   tools/store_policy_probe [rounds=4] [reps=10] [stripes=4096]
 #include <hip/hip_runtime.h>
 
