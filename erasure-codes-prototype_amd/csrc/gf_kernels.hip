@@ -441,7 +441,13 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const LatA
     if (live) {
 #pragma unroll
         for (int p = 0; p < MT; ++p)
-            if (p < nrows) __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(dst[p] + off));
+            if (p < nrows) {
+#ifdef ECG_TUNE_LAT_STORE_SC1  // tuning builds only (tools/build_variant.sh): write-through output stores
+                asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(dst[p] + off), "v"(acc[p]) : "memory");
+#else
+                __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(dst[p] + off));
+#endif
+            }
     }
     if (flags) post_done_flag(flags + blockIdx.x, a.done_seq);
 }

@@ -21,8 +21,8 @@
 #              form) -> workload_profile.json (tools/workload_profile.py; copy it to profiles/ for bench.py)
 #   ceiling    tools/movement_ceiling: the product kernel's own access path with the multiply removed, and its
 #              rocprofv3 kernel stats                                             -> ceiling.txt, ceiling_prof/
-#   abrepair   config 3's per-call forms (1 and 8 threads), the tree's libecg vs lib/ab/ (ECG_LIB), alternated
-#              over 3 rounds                                                       -> abrepair_<v>_<r>.log
+#   abrepair   config 3's per-call forms (1 and 8 threads), the tree's libecg vs $AB_LIB (default lib/ab/libecg.so;
+#              loaded through ECG_LIB), alternated over 3 rounds                  -> abrepair_<v>_<r>.log
 #   callrate   tools/call_rate + tools/record_cost (device-tier per-call cost)     -> call_rate.txt, record_cost.txt
 #   ab         per-call cost A/B: the tree's libecg vs erasure-codes-prototype_amd/lib/ab/ (a build of an earlier
 #              commit), tools/call_rate device + tools/record_cost, alternated over 3 rounds -> ab_<v>_<r>.txt
@@ -121,7 +121,7 @@ for step in "$@"; do
              rc=$?; echo "ceiling prof rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     abrepair) for r in 1 2 3; do
                 for v in new prev; do
-                  if [ $v = prev ]; then EL=$R/erasure-codes-prototype_amd/lib/ab/libecg.so; else EL=$R/erasure-codes-prototype_amd/lib/libecg.so; fi
+                  if [ $v = prev ]; then EL=${AB_LIB:-$R/erasure-codes-prototype_amd/lib/ab/libecg.so}; else EL=$R/erasure-codes-prototype_amd/lib/libecg.so; fi
                   run "lrc per-call $v $r" 300 "$O/abrepair_${v}_$r.log" env ECG_LIB=$EL python bench.py --workload lrc-repair \
                     --forms reference_sequence_per_call,reference_sequence_per_call_threads8 --steps 10 --warmup 2 --no-cpu-baseline
                 done
