@@ -404,6 +404,19 @@ __device__ __forceinline__ void lat_fold_lds(const int k, const CoefTab* T, cons
     }
 }
 
+// The latency kernel's output stores are non-temporal.  Write-through stores (`sc0 sc1`: the line leaves the
+// XCD's L2 with the store, so the end-of-kernel release and the flag epilogue's L2 write-back find nothing
+// dirty) were tried for single calls: config 3's per-call sequence A/B over two boxes went 0.119-0.135 ->
+// 0.135-0.141 on one and 0.124-0.145 -> 0.123-0.131 on the other, i.e. within the spread
+// (profiles/r05/percall_args/latsc1/).  ECG_TUNE_LAT_STORE_SC1 builds them (tuning builds only).
+__device__ __forceinline__ void lat_store(uint32_t* p, uint32_t v) {
+#ifdef ECG_TUNE_LAT_STORE_SC1
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+#else
+    __builtin_nontemporal_store(v, p);
+#endif
+}
+
 // EAGER (blocks <= kLatEagerBytes): a scheduling barrier keeps every input load ahead of the fold.  RS(6,4)
 // 1 KiB host calls 0.3-2 us faster (A/B of two builds over two boxes, profiles/r02/lat_kernel/eager/);
 // single device calls at 64 KiB - 1 MiB measured 1-5 % slower with it, so only small blocks take it.
@@ -441,13 +454,7 @@ __global__ void __launch_bounds__(kLatThreads, 1) gf_lat_dword_kernel(const LatA
     if (live) {
 #pragma unroll
         for (int p = 0; p < MT; ++p)
-            if (p < nrows) {
-#ifdef ECG_TUNE_LAT_STORE_SC1  // tuning builds only (tools/build_variant.sh): write-through output stores
-                asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(dst[p] + off), "v"(acc[p]) : "memory");
-#else
-                __builtin_nontemporal_store(acc[p], reinterpret_cast<uint32_t*>(dst[p] + off));
-#endif
-            }
+            if (p < nrows) lat_store(reinterpret_cast<uint32_t*>(dst[p] + off), acc[p]);
     }
     if (flags) post_done_flag(flags + blockIdx.x, a.done_seq);
 }
