@@ -472,7 +472,7 @@ def rs_encode_decode(a, r):
 WORKLOAD_PROFILE = os.path.join(ROOT, "profiles", "workload_profile.json")
 CONFIG3_FORMS = ("fused", "reference_sequence_scope_scratch", "reference_sequence_per_call",
                  "reference_sequence_per_call_threads8")
-CONFIG4_FORMS = ("rows", "fused")
+CONFIG4_FORMS = ("rows", "fused", "reference_sequence_scope_scratch", "reference_sequence_per_call")
 
 
 def workload_profile(key):
@@ -597,8 +597,10 @@ def config3_cpu_baseline(a):
 def config4_line(a, r):
     """BASELINE.json configs[3] in the default line: PC(4,1,4,1), 4 MiB blocks, stripe merging x = 2
     (HORIZONTAL), 512 merges per GPU (pc_merge): the row form (each merged row parity one 8 -> 1 XOR launch
-    stripe) and the fused 40 -> 5 call the engine splits into rows.  Rank 0 at N = 1 adds the oracle's CPU
-    run of the same row calls."""
+    stripe), the fused 40 -> 5 call the engine splits into rows, and the proxies' own per-row sequence
+    (helper partial, main partial, perform_addition; merge.cpp:1310-1402) in batch scopes with the partials
+    declared scratch and one call at a time.  Rank 0 at N = 1 adds the oracle's CPU run of the same per-row
+    call sequence."""
     try:
         torch.cuda.empty_cache()
         res = pc_merge(a, r, only=CONFIG4_FORMS, steps=min(a.steps, 10), warmup=min(a.warmup, 2),
@@ -621,26 +623,30 @@ def config4_line(a, r):
 
 
 def config4_cpu_baseline(a):
-    """The same merges on the CPU: per merge, 5 calls jerasure_matrix_encode(8, 1, all ones) over the row's
-    8 blocks of the two old stripes (blocks [2][25] per merge, PC(4,1,4,1) rowcol2bid, pc.cpp:326-340)."""
+    """The same merges on the CPU as the proxies compute them: per merged row, the helper's partial and the
+    main proxy's partial (jerasure_matrix_encode(4, 1, ones) over each old stripe's 4 row blocks) and
+    perform_addition of the two (handle_merge.cpp:269-270,319,453-454; pc_merge_plan), blocks [2][25] per
+    merge (PC(4,1,4,1) rowcol2bid, pc.cpp:326-340)."""
     import numpy as np
     B, nb = 4 << 20, 50
-
-    def bid(row, col):
-        return row * 4 + col if row < 4 else 20 + col
-    calls = [(nb + row, [half * 25 + bid(row, col) for half in range(2) for col in range(4)], [1] * 8)
-             for row in range(5)]
+    main_blocks, _, _, help_blocks, _, _ = pc_merge_plan(25)
+    calls = []
+    for row in range(5):
+        calls += [(nb + 5, [int(x) for x in help_blocks[row]], [1] * 4),
+                  (nb + 6, [int(x) for x in main_blocks[row]], [1] * 4),
+                  (nb + row, [nb + 5, nb + 6], [1, 1])]
     threads, _ = host_cpus()
     S = threads  # 200 MiB per merge: 3.2 GiB of host memory at 16 threads
-    t, reps, threads, facts, blocks, out = seq_cpu_baseline(nb, 5, B, [calls], None, a.cpu_seconds / 4, 0, S)
+    t, reps, threads, facts, blocks, out = seq_cpu_baseline(nb, 5, B, [calls], None, a.cpu_seconds / 4, 2, S)
     ok = True
-    for row, (_, src, _) in enumerate(calls):
+    for row in range(5):
+        src = list(main_blocks[row]) + list(help_blocks[row])
         ok &= bool(np.array_equal(out[:, row], np.bitwise_xor.reduce(blocks[:, src], axis=1)))
     return {"value": round(reps * S * 45 * B / t / 1e9, 3), "unit": "GB/s of algorithmic bytes (9 * B per row)",
             "merges_per_s": round(reps * S / t, 1), "cores": threads, "kind": "port", "threads_used": threads,
             **facts, "verified": ok,
-            "sample": f"{reps} x {S} merges (5 row calls jerasure_matrix_encode(8, 1, ones) each), {threads} host "
-                      f"threads, {t:.1f} s"}
+            "sample": f"{reps} x {S} merges (per row: helper partial, main partial, perform_addition -- three "
+                      f"jerasure_matrix_encode calls), {threads} host threads, {t:.1f} s"}
 
 
 def optional_deadline_s() -> float:
@@ -984,8 +990,8 @@ _REPLAY = None
 
 
 def replay_lib():
-    """libecg_replay.so (loopback/replay.cpp, built with libecg): the proxy's per-stripe repair calls
-    issued from C++ through the C ABI."""
+    """libecg_replay.so (loopback/replay.cpp, built with libecg): the proxies' per-stripe repair and merge
+    calls issued from C++ through the C ABI."""
     global _REPLAY
     if _REPLAY is None:
         import ctypes
@@ -997,6 +1003,8 @@ def replay_lib():
         L.ecg_replay_partial_repair.restype = I
         L.ecg_replay_partial_repair_mt.argtypes = [P, P, I, I, I, P, LL, LL, I, I, P, P, P, I, P, I, P, I, P, P, P, LL]
         L.ecg_replay_partial_repair_mt.restype = I
+        L.ecg_replay_merge.argtypes = [P, P, I, I, P, LL, LL, I, I, I, I, P, P, P, I, P, P, P, P, P, LL, LL, P]
+        L.ecg_replay_merge.restype = I
         L.ecg_replay_host_encode.argtypes = [I, I, P, P, P, I, I, I, I]
         L.ecg_replay_host_encode.restype = I
         _REPLAY = L
@@ -1198,12 +1206,38 @@ def lrc_repair_ring(a, r):
 
 # ------------------------------------------------------------------------------- config 4
 
+def pc_merge_plan(nb=25):
+    """The per-row calls of config 4's merge as the proxies issue them (merge.cpp:1310-1402): the old stripes'
+    blocks are [2][nb] per merge (PC(4,1,4,1) rowcol2bid, pc.cpp:326-340: data (r<4, c<4) = 4r + c, column
+    parity (4, c) = 20 + c).  Row r's helper (help_recal over old stripe 2, a PC(8,1,4,1) handle) takes the
+    merged-stripe block ids of its 4 blocks -- columns 4..7 of row r: 8r + 4 + c, or 36 + 4 + c in the
+    column-parity row -- and the new row parity's id (32 + r, or 44 = G); the main proxy (main_recal over old
+    stripe 1, an RS(8,1) row-code handle) takes columns 0..3 and parity column 8.  Returns int32 arrays
+    (main_blocks, main_cols, main_parity, help_blocks, help_ids, help_parity), one row per merged row."""
+    import numpy as np
+
+    def old_bid(row, col):
+        return row * 4 + col if row < 4 else 20 + col
+
+    def new_bid(row, col):  # PC(8,1,4,1): data 8r + c, R(r) = 32 + r, C(c) = 36 + c, G = 44
+        if col == 8:
+            return 32 + row if row < 4 else 44
+        return row * 8 + col if row < 4 else 36 + col
+    rows = range(5)
+    main_blocks = [[old_bid(r, c) for c in range(4)] for r in rows]
+    help_blocks = [[nb + old_bid(r, c) for c in range(4)] for r in rows]
+    help_ids = [[new_bid(r, 4 + c) for c in range(4)] for r in rows]
+    arr = lambda x: np.ascontiguousarray(np.array(x, dtype=np.int32))  # noqa: E731
+    return (arr(main_blocks), arr([[0, 1, 2, 3]] * 5), arr([8] * 5), arr(help_blocks), arr(help_ids),
+            arr([new_bid(r, 8) for r in rows]))
+
+
 def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
     """PC(4,1,4,1), 4 MiB blocks, merge x=2 HORIZONTAL: merged PC(8,1,4,1) row r parity = XOR of the
     two old stripes' row-r data blocks (r < 4) / column-parity blocks (r = 4); the RS(8,1) row code is all
     ones (main_recal / help_recal, handle_merge.cpp:159,269,319,453).  One launch reads 40 blocks and
-    writes 5 per merge (the algorithmic minimum, 9 * B per row).  Three formulations are timed (below);
-    only / steps / warmup as in lrc_repair."""
+    writes 5 per merge (the algorithmic minimum, 9 * B per row).  The engine's formulations and the proxies'
+    own per-row call sequence are timed (below); only / steps / warmup as in lrc_repair."""
     steps = a.steps if steps is None else steps
     warmup = a.warmup if warmup is None else warmup
     B = B or a.block_size or (4 << 20)
@@ -1238,19 +1272,57 @@ def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
         finally:
             ecg.set_option(ecg.ECG_OPT_ROW_SPLIT, saved)
 
+    # The proxies' own per-row calls (helper partial, main partial, perform_addition; pc_merge_plan), issued
+    # from C++ through the C ABI (loopback/replay.cpp ecg_replay_merge): one call at a time (form 0), in
+    # deferred-batch scopes (1), and in scopes with the partials declared scratch (2: the three calls compose
+    # into the row's one 8 -> 1 product).  The partials buffer is allocated only when such a form runs.
+    replay_stats = {}
+    scope_merges = 64  # 320 rows, 960 recorded calls per scope
+
+    def replay(form):
+        import numpy as np
+        rp = replay_lib()
+        main_ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=8, m=1))
+        main_ec.init_coding_parameters(ecg.CodingParameters(k=8, m=1))
+        new_cp = ecg.CodingParameters(k1=8, m1=1, k2=4, m2=1)
+        help_ec = ecg.ec_factory(ecg.ECTYPE.PC, new_cp)
+        help_ec.init_coding_parameters(new_cp)
+        plan = pc_merge_plan(nb)
+        partials = torch.empty((S, 5, 2, B), dtype=torch.uint8, device="cuda")
+
+        def fn():
+            p = [x.ctypes.data for x in plan]
+            rc = rp.ecg_replay_merge(main_ec._h, help_ec._h, form, scope_merges, blocks.data_ptr(), blocks.stride(0),
+                                     blocks.stride(1), B, S, 5, 4, p[0], p[1], p[2], 4, p[3], p[4], p[5],
+                                     partials.data_ptr(), out.data_ptr(), out.stride(0), out.stride(1),
+                                     torch.cuda.current_stream().cuda_stream)
+            if rc != 0:
+                raise ecg.EcgError(rc, "ecg_replay_merge")
+            if form > 0:
+                replay_stats[form] = ecg.batch_last_stats()
+        fn.keep = (main_ec, help_ec, plan, partials, np)
+        return fn
+
     # "fused" is what a multi-row caller reaches: the engine splits the separable 40 -> 5 program into five
     # 8 -> 1 row programs by itself (ECG_OPT_ROW_SPLIT); "fused_unsplit" is the same call without the split
+    # (name -> form factory, built only when the form runs)
     variants = {
-        "rows": lambda: ecg.matrix_apply_batch_multi(rows, blocks, out, prog_of_stripe=prog_of, stripe_of=stripe_of),
-        "fused": lambda: ecg.matrix_apply_batch_multi(fused, blocks, out),
-        "fused_unsplit": unsplit,
+        "rows": lambda: lambda: ecg.matrix_apply_batch_multi(rows, blocks, out, prog_of_stripe=prog_of,
+                                                             stripe_of=stripe_of),
+        "fused": lambda: lambda: ecg.matrix_apply_batch_multi(fused, blocks, out),
+        "fused_unsplit": lambda: unsplit,
+        "reference_sequence_per_call": lambda: replay(0),
+        "reference_sequence_scope": lambda: replay(1),
+        "reference_sequence_scope_scratch": lambda: replay(2),
     }
     alg = S * 45 * B
+    per_call_bytes = S * 5 * 13 * B  # 4 + 1, 4 + 1, 2 + 1 blocks per row: the partials round-trip HBM
     res = {}
     wanted = only if only is not None else (a.forms.split(",") if a.forms else None)
-    for name, fn in variants.items():
+    for name, make in variants.items():
         if wanted is not None and name not in wanted:
             continue
+        fn = make()
         def step(ev=None, fn=fn):
             if ev:
                 ev[0].record()
@@ -1284,11 +1356,28 @@ def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
         assert ok, f"merge mismatch ({name}, device check)"
         elapsed, evs = timed_loop(r, steps, step)
         t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+        executed = alg
+        extra = {}
+        if name.startswith("reference_sequence"):
+            executed = per_call_bytes
+            extra["issued_from"] = ("C++ through the C ABI (loopback/replay.cpp ecg_replay_merge), the helper's and "
+                                    "the main proxy's partial and perform_addition per merged row")
+            if name != "reference_sequence_per_call":
+                st = replay_stats[1 if name == "reference_sequence_scope" else 2]
+                extra["last_scope_flush"] = st
+            if name == "reference_sequence_scope_scratch":
+                last = S - ((S - 1) // scope_merges) * scope_merges  # the last scope's merges
+                composed_away = (st["recorded"] == 15 * last and st["composed"] == 5 * last
+                                 and st["materialised"] == 0)
+                extra["partials_composed_away"] = composed_away
+                executed = alg if composed_away else None
         res[name] = {"ms_per_batch": round(t * 1e3, 3), "merges_per_s": round(r.world * S * steps / elapsed, 1),
                      "algorithmic_GBps": round(alg / t / 1e9, 1),
                      "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
-                     "executed_bytes_per_batch": alg, "executed_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
-                     "verified": True, "batches_run": warmup + steps}
+                     "executed_bytes_per_batch": executed,
+                     "executed_frac": round(executed / t / 1e9 / HBM_PEAK_GBS, 4) if executed else None,
+                     **extra, "verified": True, "batches_run": warmup + steps}
+        del fn
     return {"workload": "PC(4,1,4,1) merge x=2 horizontal, 4 MiB blocks", "n_gpus": r.world,
             "merges_per_gpu": S, "steps": steps, "algorithmic_bytes_per_batch": alg, "results": res,
             "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}

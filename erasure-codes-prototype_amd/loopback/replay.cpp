@@ -1,5 +1,6 @@
-// libecg_replay.so: the proxy's per-stripe repair call sequence, issued from C++ as the proxy issues it,
-// for bench.py (config 3, `--workload lrc-repair`, form "partial_decoding_scope_scratch").
+// libecg_replay.so: the proxies' per-stripe repair and merge call sequences, issued from C++ as the proxies
+// issue them, for bench.py (config 3 `--workload lrc-repair`, config 4 `--workload pc-merge`, and the line's
+// config3 / config4 objects).
 //
 // The reference's main/help repair with partial decoding makes, per stripe, three ErasureCode calls
 // (handle_repair.cpp:249,371-376,566): a helper proxy's encode_partial_blocks_for_decoding over its
@@ -96,6 +97,67 @@ int ecg_replay_partial_repair_mt(ecg_ec** ecs, void** streams, int nthreads, int
     for (auto& x : th) x.join();
     for (int rc : rcs)
         if (rc) return rc;
+    return 0;
+}
+
+// Config 4's stripe merging as the proxies issue it (merge.cpp:1310-1402): per merge and merged-stripe row,
+// the helper proxy's encode_partial_blocks_for_encoding over the old stripe it holds, through a handle of the
+// stripe's own code with merged-stripe block ids (help_recal, handle_merge.cpp:380-381,453-454; PC maps them
+// to row-code columns, pc.cpp:257-285), then the main proxy's own partial through an RS(x k1, m1) row-code
+// handle with column indices (main_plan.ec_type = RS, merge.cpp:1327-1335; handle_merge.cpp:13-14,269-270),
+// then perform_addition of the two partials into the new row parity (:319).  Merge s's blocks at
+// base + s * sstride + b * bstride; row r's helper blocks help[r * n_help ..] with ids help_idx[..] and parity
+// id help_parity[r], its main blocks main_[r * n_main ..] with columns main_idx[..] and parity column
+// main_parity[r]; the partials of (merge s, row r) at partials + ((s * rows + r) * 2 + j) * B; the new parity
+// at out + s * out_sstride + r * out_bstride.  Forms as ecg_replay_partial_repair (scopes of scope_merges
+// merges).  Asynchronous on `stream`; returns 0 or the first negative ecg_* status.
+int ecg_replay_merge(ecg_ec* main_ec, ecg_ec* help_ec, int form, int scope_merges, char* base, long long sstride,
+                     long long bstride, int B, int S, int rows, int n_main, const int* main_, const int* main_idx,
+                     const int* main_parity, int n_help, const int* help, const int* help_idx, const int* help_parity,
+                     char* partials, char* out, long long out_sstride, long long out_bstride, void* stream) {
+    if (!main_ec || !help_ec || form < 0 || form > 2 || B <= 0 || S < 0 || rows < 1 || n_main < 1 || n_help < 1 ||
+        (form > 0 && scope_merges < 1))
+        return ECG_EINVAL;
+    int rc = ecg_ec_set_memory(main_ec, ECG_MEM_DEVICE, stream);
+    if (!rc) rc = ecg_ec_set_memory(help_ec, ECG_MEM_DEVICE, stream);
+    if (rc) return rc;
+    std::vector<char*> hp(n_help), mp(n_main);
+    auto merge = [&](int s) -> int {
+        char* blk0 = base + (long long)s * sstride;
+        for (int r = 0; r < rows; r++) {
+            for (int j = 0; j < n_help; j++) hp[j] = blk0 + (long long)help[r * n_help + j] * bstride;
+            for (int j = 0; j < n_main; j++) mp[j] = blk0 + (long long)main_[r * n_main + j] * bstride;
+            char* pp[2] = {partials + ((long long)s * rows + r) * 2 * B,
+                           partials + (((long long)s * rows + r) * 2 + 1) * B};
+            int r1 = ecg_ec_encode_partial_blocks_for_encoding(help_ec, hp.data(), &pp[0], B, help_idx + r * n_help,
+                                                               n_help, help_parity + r, 1);
+            if (r1) return r1;
+            r1 = ecg_ec_encode_partial_blocks_for_encoding(main_ec, mp.data(), &pp[1], B, main_idx + r * n_main,
+                                                           n_main, main_parity + r, 1);
+            if (r1) return r1;
+            char* o = out + (long long)s * out_sstride + (long long)r * out_bstride;
+            if ((r1 = ecg_ec_perform_addition(main_ec, pp, &o, B, 2, 1))) return r1;
+        }
+        return 0;
+    };
+    if (form == 0) {
+        for (int s = 0; s < S; s++)
+            if ((rc = merge(s))) return rc;
+        return 0;
+    }
+    for (int c0 = 0; c0 < S; c0 += scope_merges) {
+        const int c1 = c0 + scope_merges < S ? c0 + scope_merges : S;
+        if ((rc = ecg_batch_begin())) return rc;
+        if (form == 2 &&
+            (rc = ecg_batch_scratch(partials + (long long)c0 * rows * 2 * B, (size_t)(c1 - c0) * rows * 2 * B))) {
+            ecg_batch_end();
+            return rc;
+        }
+        for (int s = c0; s < c1 && !rc; s++) rc = merge(s);
+        const int re = ecg_batch_end();
+        if (rc) return rc;
+        if (re) return re;
+    }
     return 0;
 }
 

@@ -328,8 +328,8 @@ def test_header_compiles_standalone():
 
 
 def test_replay_library_refuses_bad_arguments():
-    """bench.py's C++ caller of config 3's per-stripe sequence (loopback/replay.cpp) loads beside libecg and
-    refuses bad arguments before touching a device."""
+    """bench.py's C++ callers of config 3's per-stripe and config 4's per-row sequences (loopback/replay.cpp)
+    load beside libecg and refuse bad arguments before touching a device."""
     import ctypes
     import sys
     sys.argv = sys.argv[:1]
@@ -337,3 +337,4 @@ def test_replay_library_refuses_bad_arguments():
     L = bench.replay_lib()
     z = ctypes.c_void_p(0)
     assert L.ecg_replay_partial_repair(z, 0, 1, z, 0, 0, 16, 1, z, z, z, 6, z, 3, z, 3, z, z, z, 0, z) == -2
+    assert L.ecg_replay_merge(z, z, 0, 1, z, 0, 0, 16, 1, 5, 4, z, z, z, 4, z, z, z, z, z, 0, 0, z) == -2

@@ -2048,3 +2048,45 @@ def test_replay_reference_repair_sequence(ecg, oracle, torch_cuda, form):
     o.encode_partial_blocks_for_decoding([host[b] for b in hs], p0, B, hs, sv, [e])
     o.encode_partial_blocks_for_decoding([host[b] for b in ms], p1, B, ms, sv, [e])
     assert np.array_equal(p0[0] ^ p1[0], out[3].cpu().numpy())
+
+
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_replay_reference_merge_sequence(ecg, oracle, torch_cuda, form):
+    """bench.py's C++ caller of config 4's per-row sequence (loopback/replay.cpp ecg_replay_merge): per merged
+    row, the helper's partial through a PC(8,1,4,1) handle with block ids, the main partial through an
+    RS(8,1) handle with columns, and perform_addition -- one launch each (form 0), in scopes (1) and in scopes
+    with scratch partials (2) -- gives every row parity of every merge (XOR of the row's 8 blocks of the two
+    old PC(4,1,4,1) stripes), and the partials are never written in form 2."""
+    import sys
+    sys.argv = sys.argv[:1]
+    import bench
+    torch = torch_cuda
+    S, B, nb = 37, 4096 + 16, 25
+    blocks = torch.empty((S, 2 * nb, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(blocks, 0x3E6 + form)
+    main_ec = ecg.ec_factory(ecg.ECTYPE.RS, ecg.CodingParameters(k=8, m=1))
+    main_ec.init_coding_parameters(ecg.CodingParameters(k=8, m=1))
+    cp = ecg.CodingParameters(k1=8, m1=1, k2=4, m2=1)
+    help_ec = ecg.ec_factory(ecg.ECTYPE.PC, cp)
+    help_ec.init_coding_parameters(cp)
+    plan = bench.pc_merge_plan(nb)
+    partials = torch.full((S, 5, 2, B), 0x5A, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((S, 5, B), dtype=torch.uint8, device="cuda")
+    p = [x.ctypes.data for x in plan]
+    rc = bench.replay_lib().ecg_replay_merge(
+        main_ec._h, help_ec._h, form, 16, blocks.data_ptr(), blocks.stride(0), blocks.stride(1), B, S, 5, 4,
+        p[0], p[1], p[2], 4, p[3], p[4], p[5], partials.data_ptr(), out.data_ptr(), out.stride(0), out.stride(1),
+        torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, ecg.lib().ecg_last_error()
+    torch.cuda.synchronize()
+    host = blocks.cpu().numpy()
+    mb, hb = plan[0], plan[3]
+    for row in range(5):
+        want = np.bitwise_xor.reduce(host[:, list(mb[row]) + list(hb[row])], axis=1)
+        assert np.array_equal(out[:, row].cpu().numpy(), want), row
+    if form == 2:
+        assert bool((partials == 0x5A).all()), "scratch partials were written"
+        st = ecg.batch_last_stats()  # the last scope: 5 merges, 5 rows, 3 calls -> 1 each
+        assert st["recorded"] == 75 and st["composed"] == 25 and st["materialised"] == 0, st
+    else:
+        assert not bool((partials == 0x5A).all())

@@ -234,6 +234,39 @@ def test_call_sequence_baseline_matches_call_by_call(oracle):
             blocks[dst] = res[0]
         assert np.array_equal(out[s, 0], blocks[nb]), s
 
+def test_pc_merge_plan_is_the_proxies_row_sequence(oracle):
+    """bench.py's pc_merge_plan (the calls ecg_replay_merge and config 4's CPU baseline issue): the helper's
+    block ids map through PC(8,1,4,1)'s bid2rowcol (pc.cpp:342-359) to columns 4..7 of their row and the
+    parity id to that row's parity column; run through the oracle -- the helper's partial with a PC(8,1,4,1)
+    handle (pc.cpp:257-285), the main partial with an RS(8,1) handle, their XOR (perform_addition) -- every
+    merged row parity equals the XOR of the row's 8 blocks of the two old stripes."""
+    import sys
+    sys.argv = sys.argv[:1]
+    import bench
+    from oracle import ec_ref as E
+    mb, mc, mp, hb, hi, hp = bench.pc_merge_plan(25)
+    pc = E.ec_factory(E.ECTYPE.PC, E.CodingParameters(k1=8, m1=1, k2=4, m2=1))
+    pc.init_coding_parameters(E.CodingParameters(k1=8, m1=1, k2=4, m2=1))
+    rs = E.RSCode(8, 1)
+    old = E.ec_factory(E.ECTYPE.PC, E.CodingParameters(k1=4, m1=1, k2=4, m2=1))
+    old.init_coding_parameters(E.CodingParameters(k1=4, m1=1, k2=4, m2=1))
+    B = 64 + 5
+    blocks = [b for b in E.blocks(50, B, 21)]
+    for row in range(5):
+        assert [pc.bid2rowcol(int(i)) for i in hi[row]] == [(row, 4 + c) for c in range(4)]
+        assert pc.bid2rowcol(int(hp[row])) == (row, 8)
+        assert [old.bid2rowcol(int(b)) for b in mb[row]] == [(row, c) for c in range(4)]
+        assert [old.bid2rowcol(int(b) - 25) for b in hb[row]] == [(row, c) for c in range(4)]
+        assert list(mc[row]) == [0, 1, 2, 3] and mp[row] == 8
+        p0, p1 = E.zeros(1, B), E.zeros(1, B)
+        pc.encode_partial_blocks_for_encoding([blocks[b] for b in hb[row]], p0, B, [int(i) for i in hi[row]],
+                                              [int(hp[row])])
+        rs.encode_partial_blocks_for_encoding([blocks[b] for b in mb[row]], p1, B, [int(i) for i in mc[row]],
+                                              [int(mp[row])])
+        want = np.bitwise_xor.reduce(np.stack([blocks[b] for b in list(mb[row]) + list(hb[row])]), axis=0)
+        assert np.array_equal(p0[0] ^ p1[0], want), row
+
+
 # ------------------------------------------------------------- reference property tests, made live
 
 def _stripe(ec, B, seed):

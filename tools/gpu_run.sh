@@ -101,7 +101,7 @@ for step in "$@"; do
          tail -1 "$O/bench_$w.log" | cut -c1-600 ;;
     wp:*) w=${step#wp:}; prof "wprof/$w" "wprof_$w.log" --workload $w --no-cpu-baseline ;;
     w34prof) C3="fused reference_sequence_scope_scratch reference_sequence_per_call reference_sequence_per_call_threads8"
-             C4="rows fused"
+             C4="rows fused reference_sequence_scope_scratch reference_sequence_per_call"
              spec=""
              for f in $C3; do
                prof "w34/c3_$f" "w34_c3_$f.log" --workload lrc-repair --forms $f --steps 10 --warmup 2 --no-cpu-baseline
