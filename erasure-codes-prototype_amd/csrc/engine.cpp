@@ -37,6 +37,22 @@ std::atomic<Engine*> g_engines[kMaxDevices] = {};
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// One call's outputs lie apart from its inputs: none inside the span of its input blocks or the m blocks
+// just past it (where an encode into [k+m][B] stripes or an in-place decode writes).  The pointer-table
+// launch's grid-map hint (gf_kernels.hip outputs_in_stripe): speed only, never correctness.
+static bool outputs_apart(const uint8_t* const* src, int k, const uint8_t* const* dst, int m, long long B) {
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    for (int j = 0; j < k; j++) {
+        lo = std::min(lo, (uintptr_t)src[j]);
+        hi = std::max(hi, (uintptr_t)src[j] + (uintptr_t)B);
+    }
+    for (int q = 0; q < m; q++) {
+        const uintptr_t d = (uintptr_t)dst[q];
+        if (d + (uintptr_t)B > lo && d < hi + (uintptr_t)m * (uintptr_t)B) return false;
+    }
+    return true;
+}
+
 // Host-tier state: a non-blocking stream, a growable device scratch, a pinned staging area and the
 // host-batch pipeline's streams and slots.  Contexts are pooled per device and LEASED for the duration
 // of one synchronous host-tier call, so these resources are bounded by the number of calls in flight
@@ -1796,7 +1812,7 @@ int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* c
         t.cap = cap;
     }
     const uint8_t** h = (const uint8_t**)t.host;
-    bool aligned = true;
+    bool aligned = true, apart = true;
     for (int s = 0; s < S; s++) {
         for (int j = 0; j < k; j++) {
             const uint8_t* p = calls[s][op.src_ids[j]];
@@ -1808,11 +1824,12 @@ int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* c
             aligned &= aligned16(p);
             h[(size_t)S * k + (size_t)s * m + q] = p;
         }
+        if (apart) apart = outputs_apart(h + (size_t)s * k, k, h + (size_t)S * k + (size_t)s * m, m, B);
     }
     ECG_HIP(hipMemcpyAsync(t.dev, t.host, n * sizeof(void*), hipMemcpyHostToDevice, st));
     const uint8_t* const* d_src = (const uint8_t* const*)t.dev;
     uint8_t* const* d_dst = (uint8_t* const*)((const uint8_t**)t.dev + (size_t)S * k);
-    const int rc = run_ptrs(op, d_src, d_dst, S, B, aligned, st);
+    const int rc = run_ptrs(op, d_src, d_dst, S, B, aligned, st, apart);
     ECG_HIP(hipEventRecord(t.ev, st));
     t.pending = true;
     return rc;
@@ -1915,7 +1932,7 @@ int Engine::run_ptr_batch_multi(const std::vector<const LinearOp*>& ops, const s
     }
     const uint8_t** h = (const uint8_t**)t.host;
     int* hp = (int*)((uint8_t*)t.host + ptr_bytes);
-    bool aligned = true;
+    bool aligned = true, apart = true;
     for (int c = 0; c < S; c++) {
         const LinearOp& op = *ops[c];
         for (int j = 0; j < k; j++) {
@@ -1928,6 +1945,7 @@ int Engine::run_ptr_batch_multi(const std::vector<const LinearOp*>& ops, const s
             aligned &= aligned16(p);
             h[(size_t)S * k + (size_t)c * m + q] = p;
         }
+        if (apart) apart = outputs_apart(h + (size_t)c * k, k, h + (size_t)S * k + (size_t)c * m, m, B);
         hp[c] = pid[c];
     }
     ECG_HIP(hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, st));
@@ -1946,6 +1964,7 @@ int Engine::run_ptr_batch_multi(const std::vector<const LinearOp*>& ops, const s
     a.MT = ps->MT;
     a.rtiles = ps->rtiles;
     a.binary = ps->binary ? 1 : 0;
+    a.grid_map = apart ? 2 : 0;  // the auto map's layout hint (gf_kernels.hip outputs_in_stripe)
     const hipError_t e = launch_gf(a, GF_MODE_PTRS, aligned, st);
     if (e != hipSuccess) {
         set_last_error(std::string("launch_gf(pointer table, multi): ") + hipGetErrorString(e));
@@ -2600,7 +2619,7 @@ int Engine::run_strided(const std::vector<LinearOp>& progs, const int* d_prog_of
 }
 
 int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
-                     bool aligned, hipStream_t st) {
+                     bool aligned, hipStream_t st, bool apart) {
     if (S < 0 || B < 0) return ECG_EINVAL;
     if (S == 0 || B == 0) return ECG_OK;
     if (!d_src || !d_dst) return ECG_EINVAL;
@@ -2622,6 +2641,7 @@ int Engine::run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t*
     a.MT = ps->MT;
     a.rtiles = ps->rtiles;
     a.binary = ps->binary ? 1 : 0;
+    a.grid_map = apart ? 2 : 0;  // the auto map's layout hint (gf_kernels.hip outputs_in_stripe)
     ECG_HIP(launch_gf(a, GF_MODE_PTRS, aligned, st));
     note_launch(*ps, st);
     return ECG_OK;

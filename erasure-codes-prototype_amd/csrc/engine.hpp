@@ -120,8 +120,9 @@ public:
                     const void* in_base, long long in_sstride, long long in_bstride, void* out_base,
                     long long out_sstride, long long out_bstride, long long B, hipStream_t stream,
                     const int* d_stripe_of = nullptr);
+    // apart: every call's outputs lie apart from its inputs (the grid-map hint, outputs_apart)
     int run_ptrs(const LinearOp& prog, const uint8_t* const* d_src, uint8_t* const* d_dst, int S, long long B,
-                 bool aligned16, hipStream_t stream);
+                 bool aligned16, hipStream_t stream, bool apart = false);
     // One op over S calls' block pointers (host arrays): uploads the pointer tables, then run_ptrs.
     int run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* const*>& call_blocks, long long B,
                       hipStream_t stream);

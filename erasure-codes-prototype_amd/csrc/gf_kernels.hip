@@ -853,8 +853,11 @@ int set_option(int opt, long long value) {
 // Grid-map auto rule (profiles/r01/shape_sweep.py, every k_in x m_out shape): when the outputs are blocks
 // of the input stripes themselves (encode: [S][k+m][B]), XCD-contiguous chunks (map 1) are 1-3 % faster;
 // when they go to a separate buffer (decode / repair / merge outputs), putting stripe s on XCD s % 8
-// (map 2) is 2-6 % faster.  Pointer-table launches have no single layout and take map 1.
+// (map 2) is 2-6 % faster.  Pointer-table launches have no single layout: the engine, which builds the
+// table, passes grid_map = 2 when every call's outputs lie apart from its inputs (a batch scope's repairs
+// and merges: 2-3 % faster in one process on the same buffers, profiles/r05/ptrs_map/), else they take map 1.
 static bool outputs_in_stripe(const GfLaunch& a, int mode) {
+    if (mode == GF_MODE_PTRS) return a.grid_map != 2;
     if (mode != GF_MODE_STRIDED) return true;
     const uint8_t* o = a.out_base;
     return a.out_sstride == a.in_sstride && o >= a.in_base && o < a.in_base + a.in_sstride;

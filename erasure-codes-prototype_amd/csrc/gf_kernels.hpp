@@ -69,7 +69,9 @@ struct GfLaunch {
     int k, m, S;
     int MT, rtiles;
     int binary;          // every coefficient is 0 or 1 -> BINARY kernel flavour
-    int grid_map;        // 0 linear, 1 XCD-contiguous workgroup -> chunk mapping, 2 stripe groups per XCD
+    int grid_map;        // 0 linear, 1 XCD-contiguous workgroup -> chunk mapping, 2 stripe groups per XCD.
+                         // launch_gf sets it; on entry, for GF_MODE_PTRS only, 2 tells the auto rule that
+                         // every call's outputs lie apart from its inputs (engine.cpp outputs_apart)
     int map_group;       // grid_map 2: G adjacent stripes per XCD group (S % (8 G) == 0)
     int wg_per_stripe;
     int cols_per_wg;     // 16-byte columns per workgroup (vector path) / bytes per workgroup (byte path)
