@@ -2,7 +2,7 @@
 concurrency under ThreadSanitizer (CPU only; the TSan tests are at the end).
 
 tools/sanitize_host.sh rebuilds every host translation unit of libecg with -fsanitize=address,undefined
-(the HIP kernels keep their device code; host flags go through -Xarch_host) and runs
+(the kernel file for its host side only: nothing here launches a kernel) and runs
 tests/sanitize/host_fuzz.cpp.  The driver exercises these parts over randomly drawn parameters of
 every code family:
 - the matrix builders and Gauss-Jordan;
