@@ -697,6 +697,7 @@ void init_options() {
     g_opt[ECG_OPT_CALL_WORKER].store(env("ECG_CALL_WORKER", 0));
     g_opt[ECG_OPT_ROW_SPLIT].store(env("ECG_ROW_SPLIT", 16));
     g_opt[ECG_OPT_GRAVEYARD].store(env("ECG_GRAVEYARD", 16384));
+    g_opt[ECG_OPT_MT1_LDS_PAD].store(env("ECG_MT1_LDS_PAD", -1));
     g_opt_init.store(1, std::memory_order_release);
 }
 
@@ -711,10 +712,16 @@ struct NoDeduce {
 };
 
 template <typename... P>
+hipError_t launch_kernel_lds(void (*kernel)(P...), dim3 grid, dim3 block, unsigned lds, hipStream_t st,
+                             typename NoDeduce<P>::type... args) {
+    void* argv[] = {(void*)&args...};
+    return hipLaunchKernel((const void*)kernel, grid, block, argv, lds, st);
+}
+
+template <typename... P>
 hipError_t launch_kernel(void (*kernel)(P...), dim3 grid, dim3 block, hipStream_t st,
                          typename NoDeduce<P>::type... args) {
-    void* argv[] = {(void*)&args...};
-    return hipLaunchKernel((const void*)kernel, grid, block, argv, 0, st);
+    return launch_kernel_lds(kernel, grid, block, 0, st, args...);
 }
 
 template <typename F>
@@ -722,9 +729,27 @@ hipError_t launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
     return launch_kernel(kernel, grid, dim3(kThreads), st, a);
 }
 
+// Single-output vector launches reserve dynamic LDS they never touch: the only effect is a cap on how many
+// of their workgroups share a CU, and with it on how many block streams a CU keeps open at once.  The best
+// cap falls as the input count grows (profiles/r05/occupancy/shapes_b4.log: k -> 1 over 1 MiB blocks, one
+// process, same buffers): 2-3 inputs +1-3 % at 12 KiB, 6 inputs +1-2 % at 20 KiB, 8-16 inputs +2-6 % at
+// 22-24 KiB; one step past each value the rate falls off a cliff.  Multi-output launches (the encode) lose
+// at every pad and take none.
+unsigned mt1_lds_pad(int k) {
+    const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
+    if (opt >= 0) return (unsigned)opt;
+    if (k <= 3) return 12288;
+    if (k == 4) return 16384;
+    if (k == 5) return 0;
+    if (k == 6) return 20480;
+    if (k == 7 || k == 9 || k == 10) return 22528;
+    return 24576;
+}
+
 template <int MT, int MODE, int NT, bool BIN>
 hipError_t gen_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
-    return launch_with(gf_vec_kernel<MT, MODE, NT, BIN>, a, g, st);
+    const unsigned lds = MT == 1 ? mt1_lds_pad(a.k) : 0u;
+    return launch_kernel_lds(gf_vec_kernel<MT, MODE, NT, BIN>, g, dim3(kThreads), lds, st, a);
 }
 
 template <int MODE, int NT, bool BIN>
@@ -846,6 +871,7 @@ int set_option(int opt, long long value) {
     if (opt == ECG_OPT_CALL_WORKER && (value < 0 || value > 1000000)) return -1;  // idle limit <= 1 s
     if (opt == ECG_OPT_ROW_SPLIT && value < 0) return -1;
     if (opt == ECG_OPT_GRAVEYARD && value < 1) return -1;
+    if (opt == ECG_OPT_MT1_LDS_PAD && (value < -1 || value > 65536)) return -1;
     g_opt[opt].store(value);
     return 0;
 }

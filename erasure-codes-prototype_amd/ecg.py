@@ -42,7 +42,8 @@ ECG_OPT_LAT_DWORD_BYTES = 6
 ECG_OPT_CALL_WORKER = 7
 ECG_OPT_ROW_SPLIT = 8
 ECG_OPT_GRAVEYARD = 9
-ECG_OPT_COUNT = 10
+ECG_OPT_MT1_LDS_PAD = 10
+ECG_OPT_COUNT = 11
 ECG_MEM_HOST = 0
 ECG_MEM_DEVICE = 1
 

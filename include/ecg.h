@@ -77,7 +77,8 @@ long long ecg_host_pinned_xfer_threshold(void);
 
 /* Kernel tuning options (process-wide; defaults also settable through the environment variables
  * ECG_NT, ECG_COLS_PER_WG, ECG_GRID_MAP, ECG_ZEROCOPY_BYTES, ECG_PROGRAM_CACHE, ECG_MAP_GROUP,
- * ECG_LAT_DWORD_BYTES, ECG_CALL_WORKER).  Results never depend on them. */
+ * ECG_LAT_DWORD_BYTES, ECG_CALL_WORKER, ECG_ROW_SPLIT, ECG_GRAVEYARD, ECG_MT1_LDS_PAD).  Results never
+ * depend on them. */
 #define ECG_OPT_NT 0           /* non-temporal policy: bit 0 = loads, bit 1 = stores (default 3) */
 #define ECG_OPT_COLS_PER_WG 1  /* 16-byte columns per workgroup, multiple of 128; 0 = auto (128 = 2 KiB) */
 #define ECG_OPT_GRID_MAP 2     /* 0 = linear, 1 = XCD-contiguous, 2 = stripe s on XCD group s%8,
@@ -111,7 +112,12 @@ long long ecg_host_pinned_xfer_threshold(void);
 #define ECG_OPT_GRAVEYARD 9 /* evicted program sets allowed to wait for a stream the library is not handed
                                again (a destroyed or idle caller stream) before one device synchronize
                                frees them all (default 16384; >= 1; see ecg_program_sets_retiring) */
-#define ECG_OPT_COUNT 10
+#define ECG_OPT_MT1_LDS_PAD 10 /* bytes of (unused) LDS reserved per workgroup of single-output vector launches
+                                  (decode of one block, repairs, merges, XOR sums): caps how many of their
+                                  workgroups share a CU.  -1 = by input count (default: 12-24 KiB, 2-6 %
+                                  faster for 8-16 inputs, profiles/r05/occupancy/); 0 = no cap; else that
+                                  many bytes, at most 65536 */
+#define ECG_OPT_COUNT 11
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
 

@@ -222,6 +222,10 @@ def test_tuning_options_validation(ecg):
         assert ecg.get_option(ecg.ECG_OPT_ROW_SPLIT) == 0
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_GRAVEYARD, 0) != 0
         assert ecg.lib().ecg_set_option(ecg.ECG_OPT_GRAVEYARD, 3) == 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_MT1_LDS_PAD, -2) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_MT1_LDS_PAD, 65537) != 0
+        assert ecg.lib().ecg_set_option(ecg.ECG_OPT_MT1_LDS_PAD, 0) == 0  # no cap
+        assert ecg.get_option(ecg.ECG_OPT_MT1_LDS_PAD) == 0
     finally:
         for o, v in enumerate(saved):
             ecg.set_option(o, v)
@@ -237,6 +241,8 @@ def test_tuning_options_validation(ecg):
         assert saved[ecg.ECG_OPT_ROW_SPLIT] == 16
     if "ECG_GRAVEYARD" not in os.environ:
         assert saved[ecg.ECG_OPT_GRAVEYARD] == 16384
+    if "ECG_MT1_LDS_PAD" not in os.environ:
+        assert saved[ecg.ECG_OPT_MT1_LDS_PAD] == -1  # by input count
 
 
 @pytest.mark.parametrize("k,m,row_k_ones", [(10, 4, 1), (6, 4, 0), (6, 3, 1), (12, 4, 1)])

@@ -1126,6 +1126,49 @@ def test_tuning_options_never_change_results(ecg, oracle, torch_cuda):
             ecg.set_option(o, v)
 
 
+@pytest.mark.parametrize("k_in", [2, 4, 6, 8, 10, 16])
+def test_mt1_lds_pad_never_changes_results(ecg, oracle, torch_cuda, k_in):
+    """ECG_OPT_MT1_LDS_PAD (unused dynamic LDS on single-output vector launches, a cap on workgroups per CU):
+    auto (by input count), none, and fixed pads up to the 64 KiB limit give identical bytes for strided
+    BINARY and GENERAL k -> 1 launches and a pointer-table scope flush, equal to the oracle's."""
+    torch = torch_cuda
+    S, B = 24, 8192 + 16
+    saved = ecg.get_option(ecg.ECG_OPT_MT1_LDS_PAD)
+    d_in = torch.empty((S, k_in, B), dtype=torch.uint8, device="cuda")
+    ecg.fill_random(d_in, 700 + k_in)
+    h = d_in.cpu().numpy()
+    rows = {"binary": [1] * k_in, "general": [(11 * j + 5) % 255 + 1 for j in range(k_in)]}
+    want = {}
+    for name, row in rows.items():
+        w = []
+        for s in (0, S - 1):
+            o = [np.zeros(B, np.uint8)]
+            oracle.jerasure_matrix_encode(k_in, 1, row, [h[s, j] for j in range(k_in)], o, B)
+            w.append(o[0])
+        want[name] = w
+    try:
+        ref = {}
+        for pad in (-1, 0, 12288, 24576, 65536):
+            ecg.set_option(ecg.ECG_OPT_MT1_LDS_PAD, pad)
+            for name, row in rows.items():
+                out = torch.full((S, 1, B), 0x3C, dtype=torch.uint8, device="cuda")
+                ecg.matrix_apply_batch(row, list(range(k_in)), [0], d_in, out)
+                torch.cuda.synchronize()
+                assert np.array_equal(out[0, 0].cpu().numpy(), want[name][0]), (pad, name)
+                assert np.array_equal(out[S - 1, 0].cpu().numpy(), want[name][1]), (pad, name)
+                ref.setdefault(name, out.clone())
+                assert torch.equal(out, ref[name]), (pad, name)
+            # the same general row as per-stripe calls in a batch scope: one pointer-table launch
+            out = torch.full((S, 1, B), 0x3C, dtype=torch.uint8, device="cuda")
+            with ecg.batch():
+                for s in range(S):
+                    ecg.matrix_apply_batch(rows["general"], list(range(k_in)), [0], d_in[s:s + 1], out[s:s + 1])
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref["general"]), (pad, "scope")
+    finally:
+        ecg.set_option(ecg.ECG_OPT_MT1_LDS_PAD, saved)
+
+
 # ------------------------------------------------------------------ edge sizes: the GF(2^8) field limit, empty inputs
 
 @pytest.mark.parametrize("k,m", [(250, 6), (200, 56), (128, 128), (255, 1), (1, 255)])
