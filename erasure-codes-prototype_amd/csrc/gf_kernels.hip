@@ -731,13 +731,15 @@ hipError_t launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
 
 // Single-output vector launches reserve dynamic LDS they never touch: the only effect is a cap on how many
 // of their workgroups share a CU, and with it on how many block streams a CU keeps open at once.  The best
-// cap falls as the input count grows (profiles/r05/occupancy/shapes_b4.log: k -> 1 over 1 MiB blocks, one
-// process, same buffers): 2-3 inputs +1-3 % at 12 KiB, 6 inputs +1-2 % at 20 KiB, 8-16 inputs +2-6 % at
-// 22-24 KiB; one step past each value the rate falls off a cliff.  Multi-output launches (the encode) lose
-// at every pad and take none.
+// cap falls as the input count grows (profiles/r05/occupancy/shapes_b4.log, shapes_k123.log: k -> 1 over
+// 1 MiB blocks, one process, same buffers): 2-3 inputs +2-4 % at 12 KiB, 6 inputs +1-2 % at 20 KiB, 8-16
+// inputs +2-6 % at 22-24 KiB; one step past each value the rate falls off a cliff (a 1 -> 1 copy already
+// at 12 KiB: 0.80 -> 0.69, so it takes none).  Multi-output launches (the encode) lose at every pad and
+// take none.
 unsigned mt1_lds_pad(int k) {
     const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
     if (opt >= 0) return (unsigned)opt;
+    if (k <= 1) return 0;
     if (k <= 3) return 12288;
     if (k == 4) return 16384;
     if (k == 5) return 0;
