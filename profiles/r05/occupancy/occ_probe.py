@@ -3,7 +3,8 @@ the rotating 1-erasure decode into the arena's rebuild blocks, as bench.py lays 
 libecg variant in rotation (ABBA over ROUNDS rounds).  libecg_ldsN.so launches every kernel with N bytes
 of unused dynamic LDS (build_lds_variants.sh): at most floor(160 KiB / N) workgroups per CU.  Every
 variant's parities and rebuilt blocks are compared with the product library's.
-usage: python occ_probe.py ROUNDS lib1 lib2 ...   (paths relative to erasure-codes-prototype_amd/lib)"""
+usage: python occ_probe.py ROUNDS lib1[:OPT=V,...] lib2 ...   (paths relative to erasure-codes-prototype_amd/lib;
+options set in that library only)"""
 import json
 import os
 import sys
@@ -16,9 +17,13 @@ import torch  # noqa: E402
 rounds, names = int(sys.argv[1]), sys.argv[2:]
 libdir = os.path.join(ROOT, "erasure-codes-prototype_amd", "lib")
 libs = {}
-for n in names:
-    ecg.LIB_PATH, ecg._L = os.path.join(libdir, n), None
+for n in names:  # "lib.so" or "lib.so:OPT=V,OPT=V" (ECG_OPT_* set in that library only)
+    path, _, opts = n.partition(":")
+    ecg.LIB_PATH, ecg._L = os.path.join(libdir, path), None
     libs[n] = ecg.lib()
+    for kv in filter(None, opts.split(",")):
+        o, v = kv.split("=")
+        ecg.set_option(int(o), int(v))
 k, m, B, S = 10, 4, 1 << 20, 4096
 n_ = k + m
 M = ecg.reed_sol_vandermonde_coding_matrix(k, m)
