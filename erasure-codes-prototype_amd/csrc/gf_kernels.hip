@@ -734,23 +734,24 @@ hipError_t launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
 // cap falls as the input count grows (profiles/r05/occupancy/shapes_b4.log, shapes_k123.log: k -> 1 over
 // 1 MiB blocks, one process, same buffers): 2-3 inputs +2-4 % at 12 KiB, 6 inputs +1-2 % at 20 KiB, 8-16
 // inputs +2-6 % at 22-24 KiB; one step past each value the rate falls off a cliff (a 1 -> 1 copy already
-// at 12 KiB: 0.80 -> 0.69, so it takes none).  Multi-output launches (the encode) lose at every pad and
-// take none.
-unsigned mt1_lds_pad(int k) {
+// at 12 KiB: 0.80 -> 0.69, so it takes none).  Six-input pointer-table launches (config 3's scope flushes)
+// do best one step higher than strided ones (+1.2-1.5 %, sweep_c3_box2.log, box3/sweep_c3.log).
+// Multi-output launches (the encode) lose at every pad and take none.
+unsigned mt1_lds_pad(int k, bool ptrs) {
     const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
     if (opt >= 0) return (unsigned)opt;
     if (k <= 1) return 0;
     if (k <= 3) return 12288;
     if (k == 4) return 16384;
     if (k == 5) return 0;
-    if (k == 6) return 20480;
+    if (k == 6) return ptrs ? 22528 : 20480;
     if (k == 7 || k == 9 || k == 10) return 22528;
     return 24576;
 }
 
 template <int MT, int MODE, int NT, bool BIN>
 hipError_t gen_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
-    const unsigned lds = MT == 1 ? mt1_lds_pad(a.k) : 0u;
+    const unsigned lds = MT == 1 ? mt1_lds_pad(a.k, MODE == GF_MODE_PTRS) : 0u;
     return launch_kernel_lds(gf_vec_kernel<MT, MODE, NT, BIN>, g, dim3(kThreads), lds, st, a);
 }
 
