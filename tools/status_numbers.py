@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The status numbers DESIGN.md §0, README.md and BASELINE.md quote, read from one final pass.
 
-    python tools/status_numbers.py [profiles/r05/final6]
+    python tools/status_numbers.py [profiles/r05/final7]
 
 Prints the bench line's headline figures, the committed headline profile and PMC traffic, config 5, the
 host path, configs 3 and 4 (with the committed per-form profile when present) and the GPU-suite tally, each
@@ -13,7 +13,7 @@ import sys
 
 
 def main():
-    d = sys.argv[1] if len(sys.argv) > 1 else "profiles/r05/final6"
+    d = sys.argv[1] if len(sys.argv) > 1 else "profiles/r05/final7"
     line = json.loads(open(os.path.join(d, "bench.log")).read().strip().splitlines()[-1])
     prof = json.load(open(os.path.join(d, "headline_profile.json")))
     pmc = json.load(open(os.path.join(d, "pmc_traffic.json")))
