@@ -277,18 +277,21 @@ def test_bench_stalled_rank_fails_within_dist_timeout():
 def test_bench_optional_section_deadline_keeps_the_line():
     """A sub-object of the line that hangs on one rank (injected: ECG_BENCH_TEST_STALL_OPTIONAL, the other
     rank waits for it in a collective) must not cost the line: every rank's optional-section deadline
-    (0.8 x ECG_DIST_TIMEOUT_S) fires before the collective timeout would abort the ranks, rank 0 prints the
-    line with an error object for the unfinished key, and every rank exits 0."""
+    (ECG_BENCH_OPTIONAL_DEADLINE_S, below the collective timeout) fires first, rank 0 prints the
+    line with an error object for the unfinished key, and every rank exits 0.  The collective timeout is
+    generous (rank start-up -- importing torch -- can take long on a loaded machine) and the optional
+    deadline is set below it explicitly."""
     import json
     import subprocess
     import time
     t0 = time.time()
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
-                        "--timeout", "200"], capture_output=True, text=True, timeout=300, cwd=ROOT,
-                       env=_bench_env(ECG_BENCH_TEST_STALL_OPTIONAL="1", ECG_DIST_TIMEOUT_S="20"))
+                        "--timeout", "250"], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=_bench_env(ECG_BENCH_TEST_STALL_OPTIONAL="1", ECG_DIST_TIMEOUT_S="120",
+                                      ECG_BENCH_OPTIONAL_DEADLINE_S="10"))
     took = time.time() - t0
     assert p.returncode == 0, (p.returncode, p.stderr[-2000:])
-    assert took < 100, took
+    assert took < 200, took
     lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
     assert lines[0]["n_gpus"] == 2 and len(lines[0]["ranks"]) == 2
@@ -296,8 +299,8 @@ def test_bench_optional_section_deadline_keeps_the_line():
     assert lines[0].get("optional_deadline_hit") is True
     # without the stall the same section completes
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
-                        "--timeout", "200"], capture_output=True, text=True, timeout=300, cwd=ROOT,
-                       env=_bench_env(ECG_DIST_TIMEOUT_S="20"))
+                        "--timeout", "250"], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=_bench_env(ECG_DIST_TIMEOUT_S="120"))
     assert p.returncode == 0, p.stderr[-2000:]
     (line,) = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert line["optional"] == {"ok": True}
@@ -333,7 +336,7 @@ def test_bench_launcher_watchdog_kills_stuck_ranks():
                        env=_bench_env(ECG_BENCH_TEST_STALL_RANK="1", ECG_DIST_TIMEOUT_S="3000"))
     took = time.time() - t0
     assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
-    assert 15 <= took < 60, took
+    assert 15 <= took < 120, took
     assert "terminating them" in p.stderr
 
 
