@@ -519,7 +519,7 @@ def seq_cpu_baseline(nb, nout, B, patterns, pat_of, target_s, nscr, S, fill=None
         reps += 1
         if rc < 0:
             raise RuntimeError("oracle call_seq_batch_mt failed")
-    return t_total, reps, threads, facts, stripes, out
+    return t_total, reps, min(threads, S), facts, stripes, out  # threads the sample's S stripes kept busy
 
 
 def config3_line(a, r):
@@ -574,7 +574,10 @@ def config3_cpu_baseline(a):
         mn = ec.partial_decoding_matrix(sets[1], surv, [e])
         patterns.append([(n + 1, sets[0], h), (n + 2, sets[1], mn), (n, [n + 1, n + 2], [1, 1])])
     threads, _ = host_cpus()
-    S = 2 * n * max(1, (2 * threads + n - 1) // n)  # whole rounds of the 16 patterns, >= 2 per thread
+    # whole rounds of the 16 patterns, >= 2 per thread up to 16 threads: at most 64 stripes (1 GiB of host
+    # blocks) whatever the core count
+    t_ = max(1, min(threads, 16))
+    S = 2 * n * max(1, (2 * t_ + n - 1) // n)
     pat_of = np.arange(S, dtype=np.int32) % n
 
     def encode(st):  # the stripes' parities (the repairs read them)
@@ -604,7 +607,7 @@ def config4_line(a, r):
     try:
         torch.cuda.empty_cache()
         res = pc_merge(a, r, only=CONFIG4_FORMS, steps=min(a.steps, 10), warmup=min(a.warmup, 2),
-                       S=a.configs34_stripes // 8 if a.configs34_stripes else 512, B=4 << 20)
+                       S=max(1, a.configs34_stripes // 8) if a.configs34_stripes else 512, B=4 << 20)
         out = {"workload": f"PC(4,1,4,1) merge x=2 horizontal, 4 MiB blocks, {res['merges_per_gpu']} merges per GPU: "
                            "the 5 row parities of the merged PC(8,1,4,1) (BASELINE configs[3])",
                "algorithmic_bytes_per_merge": "5 rows x 9 B = 180 MiB",
@@ -636,7 +639,9 @@ def config4_cpu_baseline(a):
                   (nb + 6, [int(x) for x in main_blocks[row]], [1] * 4),
                   (nb + row, [nb + 5, nb + 6], [1, 1])]
     threads, _ = host_cpus()
-    S = threads  # 200 MiB per merge: 3.2 GiB of host memory at 16 threads
+    # 200 MiB of host stripes per merge: the sample is capped at 16 merges (3.2 GiB) whatever the core count
+    # (S = threads reached ~55 GiB on a 256-CPU host without a quota); the threads share them
+    S = max(1, min(threads, 16))
     t, reps, threads, facts, blocks, out = seq_cpu_baseline(nb, 5, B, [calls], None, a.cpu_seconds / 4, 2, S)
     ok = True
     for row in range(5):

@@ -88,6 +88,11 @@ int ecg_batch_last_stats(long long* recorded, long long* composed, long long* la
     return ECG_OK;
 }
 
+int ecg_traffic_counters(long long* launches, long long* bytes) {
+    launch_traffic(launches, bytes);
+    return ECG_OK;
+}
+
 int ecg_set_option(int option, long long value) { return set_option(option, value) == 0 ? ECG_OK : ECG_EINVAL; }
 long long ecg_get_option(int option) { return get_option(option); }
 

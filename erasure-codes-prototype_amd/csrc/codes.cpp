@@ -9,6 +9,7 @@
 
 #include "engine.hpp"
 #include "gf256.hpp"
+#include "gf_kernels.hpp"
 
 namespace ecg {
 
@@ -265,12 +266,84 @@ int ErasureCode::run_encode(int kk, int mm, const int* matrix, char** data_ptrs,
     return run(encode_plan(kk, mm, matrix), data_ptrs, kk, coding_ptrs, mm, B);
 }
 
+// ---- whole-call plans: composition and the per-thread plan cache
+//
+// A multi-step method (product-code encode: row codes, then column codes over data AND the row parities just
+// written, pc.cpp:39-76; the iterative decodes, pc.cpp:79-195, 921-1029) plans one op per sub-code call.  Run
+// as planned, each op is a launch and the column ops re-read the data and the parities the row ops wrote:
+// PC(4,1,4,1) encode moves 45 blocks for 16 in and 9 out.  compose_chain substitutes every read of a block
+// the call itself wrote with that block's expression over the call's inputs (exact, by linearity), so the
+// call becomes ONE op that reads each input once and writes each output once (25 blocks, one launch).
+// Blocks a row tile of the kernel moves: every tile reads all of its op's inputs.
+static long long op_traffic(const LinearOp& op) {
+    const int mt = op_is_binary(op) ? kMaxMTBin : kMaxMT;
+    return (long long)(op.m_out() + mt - 1) / mt * op.k_in() + op.m_out();
+}
+
+// The chain as the engine should run it: composed when that moves no more blocks than the chain and, for the
+// GENERAL flavour (straight-line dense fold, every coefficient of a tile folded even where it is 0), keeps the
+// fold within 6 coefficient products per block moved -- RS(10,4)'s encode folds 40 per 14 blocks at ~35 % of
+// gfx950's VALU issue at the HBM roofline (gf_kernels.hip header).  Otherwise the ops as planned.
+static SharedOps finish_plan(std::vector<LinearOp>&& ops) {
+    auto out = std::make_shared<std::vector<LinearOp>>();
+    LinearOp one;
+    if (ops.size() > 1 && compose_chain(ops, one)) {
+        long long chained = 0;
+        for (const LinearOp& op : ops) chained += op_traffic(op);
+        const long long moved = op_traffic(one);
+        const bool binary = op_is_binary(one);
+        const long long tiles = (one.m_out() + kMaxMT - 1) / kMaxMT;
+        const bool valu_ok = binary || (long long)one.k_in() * tiles * kMaxMT <= 6 * moved;
+        if (moved <= chained && valu_ok) {
+            out->push_back(std::move(one));
+            return out;
+        }
+    }
+    *out = std::move(ops);
+    return out;
+}
+
+namespace {
+struct CallPlan {
+    SharedOps ops;
+    int status = ECG_OK;  // the planner's status (an undecodable iterative decode still runs what it planned)
+};
+}  // namespace
+
+static KeyedCache<CallPlan>& call_plans() {
+    thread_local KeyedCache<CallPlan> cache;
+    return cache;
+}
+
+// Find the plan of the call keyed by `key` -- the exact inputs of its planning -- or make it with build(plan),
+// which returns the planner's status.  Returns that status; cp is set unless the status is an error other than
+// ECG_EUNDECODABLE (nothing is cached or run then).  An undecodable iterative decode keeps the work it planned.
+template <class Build>
+static int run_planned(const std::vector<int>& key, Build build, const CallPlan*& cp) {
+    const uint64_t h = hash_ints(key);
+    cp = call_plans().find(key, h);
+    if (cp) return cp->status;
+    Plan p;
+    const int status = build(p);
+    if (status != ECG_OK && status != ECG_EUNDECODABLE) return status;
+    cp = &call_plans().put(key, h, CallPlan{finish_plan(std::move(p.ops)), status});
+    return status;
+}
+
 int ErasureCode::run_decode(int kk, int mm, const int* matrix, int row_k_ones, int* erasures, char** data_ptrs,
                             char** coding_ptrs, long long B) {
-    Plan p;
-    int rc = append_decode(p, kk, mm, matrix, row_k_ones, erasures, iota_ids(kk), iota_ids(mm, kk));
-    if (rc != ECG_OK) return rc;
-    return run(p, data_ptrs, kk, coding_ptrs, mm, B);
+    // keyed by everything plan_matrix_decode reads: shape, flag, matrix entries, the -1-terminated erasures
+    thread_local std::vector<int> key;
+    key.assign({6, kk, mm, row_k_ones});
+    key.insert(key.end(), matrix, matrix + (size_t)kk * mm);
+    for (int i = 0; erasures[i] != -1; i++) key.push_back(erasures[i]);  // the planner reads up to the -1 too
+    const CallPlan* cp = nullptr;
+    const int rc = run_planned(key, [&](Plan& p) {
+        return append_decode(p, kk, mm, matrix, row_k_ones, erasures, iota_ids(kk), iota_ids(mm, kk));
+    }, cp);
+    if (rc != ECG_OK) return rc;  // the library decodes nothing when it returns -1
+
+    return run(cp->ops, data_ptrs, kk, coding_ptrs, mm, B);
 }
 
 // Per-thread cache of the partial calls' plans, keyed by the object's state_key and the call's index
@@ -959,23 +1032,31 @@ std::vector<std::vector<int>> ProductCode::block_map() const {
     return bm;
 }
 
-int ProductCode::encode(char** data_ptrs, char** coding_ptrs, int block_size) {  // pc.cpp:39-76
-    Plan p;
-    for (int i = 0; i < k2; i++) {
-        std::vector<int> d(k1), c(m1);
-        for (int j = 0; j < k1; j++) d[j] = i * k1 + j;
-        for (int j = 0; j < m1; j++) c[j] = k + i * m1 + j;
-        int rc = rowc().plan_encode(p, d, c);
-        if (rc != ECG_OK) return rc;
-    }
-    for (int i = 0; i < k1 + m1; i++) {
-        std::vector<int> d(k2), c(m2);
-        for (int j = 0; j < k2; j++) d[j] = i < k1 ? j * k1 + i : k + j * m1 + i - k1;
-        for (int j = 0; j < m2; j++) c[j] = i < k1 ? k + k2 * m1 + j * k1 + i : k + k2 * m1 + k1 * m2 + j * m1 + i - k1;
-        int rc = colc().plan_encode(p, d, c);
-        if (rc != ECG_OK) return rc;
-    }
-    return run(p, data_ptrs, k, coding_ptrs, m, block_size);
+// The row codes, then the column codes over the data and the row parities (pc.cpp:39-76), planned as one call
+// and composed (finish_plan): each data block is read once, the row parities are not re-read.
+int ProductCode::encode(char** data_ptrs, char** coding_ptrs, int block_size) {
+    thread_local std::vector<int> key;
+    key.assign({4});
+    state_key(key);
+    const CallPlan* cp = nullptr;
+    const int rc = run_planned(key, [&](Plan& p) {
+        for (int i = 0; i < k2; i++) {
+            std::vector<int> d(k1), c(m1);
+            for (int j = 0; j < k1; j++) d[j] = i * k1 + j;
+            for (int j = 0; j < m1; j++) c[j] = k + i * m1 + j;
+            if (int r = rowc().plan_encode(p, d, c); r != ECG_OK) return r;
+        }
+        for (int i = 0; i < k1 + m1; i++) {
+            std::vector<int> d(k2), c(m2);
+            for (int j = 0; j < k2; j++) d[j] = i < k1 ? j * k1 + i : k + j * m1 + i - k1;
+            for (int j = 0; j < m2; j++)
+                c[j] = i < k1 ? k + k2 * m1 + j * k1 + i : k + k2 * m1 + k1 * m2 + j * m1 + i - k1;
+            if (int r = colc().plan_encode(p, d, c); r != ECG_OK) return r;
+        }
+        return (int)ECG_OK;
+    }, cp);
+    if (rc != ECG_OK) return rc;
+    return run(cp->ops, data_ptrs, k, coding_ptrs, m, block_size);
 }
 
 // Iterative control flow of pc.cpp:79-195 (and HVPC pc.cpp:921-1029 with ncols = k1, nrows = k2).
@@ -1044,11 +1125,26 @@ int ProductCode::plan_iterative_decode(Plan& p, int* erasures, int failed_num, i
     return ECG_OK;
 }
 
+// Iterative decode (pc.cpp:79-195) planned on the host, composed into one pass where it can be (finish_plan).
 int ProductCode::decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) {
-    Plan p;
-    const int status = plan_iterative_decode(p, erasures, failed_num, k1 + m1, k2 + m2);
-    if (status == ECG_EINVAL) return status;
-    int rc = run(p, data_ptrs, k, coding_ptrs, m, block_size);
+    return decode_iterative(data_ptrs, coding_ptrs, block_size, erasures, failed_num, k1 + m1, k2 + m2);
+}
+
+int ProductCode::decode_iterative(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num,
+                                  int ncols, int nrows) {
+    const int nf = std::max(0, failed_num);
+    thread_local std::vector<int> key;
+    key.assign({5, ncols, nrows, failed_num});
+    state_key(key);
+    key.insert(key.end(), erasures, erasures + nf);
+    const CallPlan* cp = nullptr;
+    const int status = run_planned(key, [&](Plan& p) {
+        std::vector<int> er(erasures, erasures + nf);  // the planner reads the list only
+        er.push_back(-1);
+        return plan_iterative_decode(p, er.data(), failed_num, ncols, nrows);
+    }, cp);
+    if (!cp) return status;
+    const int rc = run(cp->ops, data_ptrs, k, coding_ptrs, m, block_size);
     return rc != ECG_OK ? rc : status;
 }
 
@@ -1200,30 +1296,32 @@ void HVPC::init_coding_parameters(const CodingParameters& cp) {  // pc.cpp:869-8
 }
 
 int HVPC::encode(char** data_ptrs, char** coding_ptrs, int block_size) {  // pc.cpp:890-918
-    Plan p;
-    for (int i = 0; i < k2; i++) {
-        std::vector<int> d(k1), c(m1);
-        for (int j = 0; j < k1; j++) d[j] = i * k1 + j;
-        for (int j = 0; j < m1; j++) c[j] = k + i * m1 + j;
-        int rc = row_code.plan_encode(p, d, c);
-        if (rc != ECG_OK) return rc;
-    }
-    for (int i = 0; i < k1; i++) {
-        std::vector<int> d(k2), c(m2);
-        for (int j = 0; j < k2; j++) d[j] = j * k1 + i;
-        for (int j = 0; j < m2; j++) c[j] = k + k2 * m1 + j * k1 + i;
-        int rc = col_code.plan_encode(p, d, c);
-        if (rc != ECG_OK) return rc;
-    }
-    return run(p, data_ptrs, k, coding_ptrs, m, block_size);
+    thread_local std::vector<int> key;
+    key.assign({4});
+    state_key(key);
+    const CallPlan* cp = nullptr;
+    const int rc = run_planned(key, [&](Plan& p) {
+        for (int i = 0; i < k2; i++) {
+            std::vector<int> d(k1), c(m1);
+            for (int j = 0; j < k1; j++) d[j] = i * k1 + j;
+            for (int j = 0; j < m1; j++) c[j] = k + i * m1 + j;
+            if (int r = row_code.plan_encode(p, d, c); r != ECG_OK) return r;
+        }
+        for (int i = 0; i < k1; i++) {
+            std::vector<int> d(k2), c(m2);
+            for (int j = 0; j < k2; j++) d[j] = j * k1 + i;
+            for (int j = 0; j < m2; j++) c[j] = k + k2 * m1 + j * k1 + i;
+            if (int r = col_code.plan_encode(p, d, c); r != ECG_OK) return r;
+        }
+        return (int)ECG_OK;
+    }, cp);
+    if (rc != ECG_OK) return rc;
+    return run(cp->ops, data_ptrs, k, coding_ptrs, m, block_size);
 }
 
+// pc.cpp:921-1029: the iterative decode over the k1 data columns and k2 data rows only
 int HVPC::decode(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num) {
-    Plan p;
-    const int status = plan_iterative_decode(p, erasures, failed_num, k1, k2);
-    if (status == ECG_EINVAL) return status;
-    int rc = run(p, data_ptrs, k, coding_ptrs, m, block_size);
-    return rc != ECG_OK ? rc : status;
+    return decode_iterative(data_ptrs, coding_ptrs, block_size, erasures, failed_num, k1, k2);
 }
 
 int HVPC::check_if_decodable(const std::vector<int>& f) { return ProductCode::check_if_decodable(f); }

@@ -357,6 +357,9 @@ protected:
     virtual RSCode& partial_row() { return row_code; }
     virtual bool has_global() const { return true; }
     int plan_iterative_decode(Plan& plan, int* erasures, int failed_num, int ncols, int nrows);
+    // plan_iterative_decode through the per-thread call-plan cache, composed (codes.cpp finish_plan), and run
+    int decode_iterative(char** data_ptrs, char** coding_ptrs, int block_size, int* erasures, int failed_num,
+                         int ncols, int nrows);
     std::vector<std::vector<int>> block_map() const;  // [row][col] -> block id in data ++ coding space
 };
 

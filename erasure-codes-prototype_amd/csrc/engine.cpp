@@ -501,7 +501,7 @@ std::shared_ptr<ProgramSet> Engine::program_set(const LinearOp* progs, size_t np
     ps->nprog = np;
     ps->k = k;
     ps->m = m;
-    ps->MT = std::min(m, kMaxMT);
+    ps->MT = std::min(m, binary ? kMaxMTBin : kMaxMT);
     ps->rtiles = (m + ps->MT - 1) / ps->MT;
     ps->binary = binary;
     const size_t per_prog = (size_t)ps->rtiles * k * ps->MT;

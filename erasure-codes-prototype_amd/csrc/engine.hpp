@@ -189,8 +189,12 @@ private:
     // under rmu_: true = the graveyard outgrew ECG_OPT_GRAVEYARD (the caller then runs sync_and_free_unheld)
     bool sweep_locked(hipStream_t current, bool has_current, std::vector<std::shared_ptr<ProgramSet>>& dead);
     size_t sync_and_free_unheld();
+    // Stream handles are 16-byte aligned pointers (their low 4 bits carry nothing); hipStreamPerThread keys
+    // (stream_key: serial << 1 | 1) are small odd numbers whose information sits in the low bits, so they
+    // are hashed whole -- shifted like handles, threads 1-7 all landed on the null stream's bit.
     static uint64_t stream_bit(hipStream_t st) {
-        return 1ull << ((((uintptr_t)st >> 4) * 0x9E3779B97F4A7C15ull) >> 58);
+        const uintptr_t v = (uintptr_t)st;
+        return 1ull << ((((v & 1) ? v : v >> 4) * 0x9E3779B97F4A7C15ull) >> 58);
     }
     // Device memory of program tables comes from a pool of power-of-two blocks, so a steady stream of new
     // programs (a proxy's open set of repair matrices) neither allocates nor frees device memory --

@@ -169,7 +169,7 @@ constexpr int occupancy_for(int MT) {
 #ifdef ECG_OCC_OVERRIDE
     return MT <= 4 ? ECG_OCC_OVERRIDE : 4;
 #else
-    return MT <= 2 ? 8 : MT <= 4 ? 6 : MT == 5 ? 3 : 4;
+    return MT <= 2 ? 8 : MT <= 4 ? 6 : MT == 5 ? 3 : 4;  // MT 9-16 (BINARY only): 64 accumulator VGPRs at 16
 #endif
 }
 
@@ -766,8 +766,23 @@ Launcher gen_pick(int MT) {
         case 6: return gen_launch<6, MODE, NT, BIN>;
         case 7: return gen_launch<7, MODE, NT, BIN>;
         case 8: return gen_launch<8, MODE, NT, BIN>;
-        default: return nullptr;
+        default: break;
     }
+    // wide BINARY tiles (kMaxMTBin): only the default NT policy is built (launch_gf runs them with it)
+    if constexpr (BIN && NT == 3) {
+        switch (MT) {
+            case 9: return gen_launch<9, MODE, NT, BIN>;
+            case 10: return gen_launch<10, MODE, NT, BIN>;
+            case 11: return gen_launch<11, MODE, NT, BIN>;
+            case 12: return gen_launch<12, MODE, NT, BIN>;
+            case 13: return gen_launch<13, MODE, NT, BIN>;
+            case 14: return gen_launch<14, MODE, NT, BIN>;
+            case 15: return gen_launch<15, MODE, NT, BIN>;
+            case 16: return gen_launch<16, MODE, NT, BIN>;
+            default: break;
+        }
+    }
+    return nullptr;
 }
 
 template <int MODE, int NT>
@@ -844,8 +859,22 @@ Launcher pick_byte_bin(int MT) {
         case 6: return byte_launch<6, MODE, BIN>;
         case 7: return byte_launch<7, MODE, BIN>;
         case 8: return byte_launch<8, MODE, BIN>;
-        default: return nullptr;
+        default: break;
     }
+    if constexpr (BIN) {
+        switch (MT) {
+            case 9: return byte_launch<9, MODE, BIN>;
+            case 10: return byte_launch<10, MODE, BIN>;
+            case 11: return byte_launch<11, MODE, BIN>;
+            case 12: return byte_launch<12, MODE, BIN>;
+            case 13: return byte_launch<13, MODE, BIN>;
+            case 14: return byte_launch<14, MODE, BIN>;
+            case 15: return byte_launch<15, MODE, BIN>;
+            case 16: return byte_launch<16, MODE, BIN>;
+            default: break;
+        }
+    }
+    return nullptr;
 }
 
 template <int MODE>
@@ -892,9 +921,20 @@ static bool outputs_in_stripe(const GfLaunch& a, int mode) {
     return a.out_sstride == a.in_sstride && o >= a.in_base && o < a.in_base + a.in_sstride;
 }
 
+// Process-wide traffic counters (ecg_traffic_counters): region-product kernels launched, and the bytes they move
+// as planned -- every row tile reads the launch's k inputs, every output is written once: S * B * (rtiles * k + m)
+// per region product.  Relaxed atomics: two uncontended adds per launch.
+std::atomic<long long> g_launched{0}, g_moved{0};
+
+void launch_traffic(long long* launches, long long* bytes) {
+    if (launches) *launches = g_launched.load(std::memory_order_relaxed);
+    if (bytes) *bytes = g_moved.load(std::memory_order_relaxed);
+}
+
 hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st, int* n_wg) {
     if (n_wg) *n_wg = 0;
-    if (base.k < 1 || base.m < 1 || base.S < 1 || base.B < 0 || base.MT < 1 || base.MT > kMaxMT)
+    if (base.k < 1 || base.m < 1 || base.S < 1 || base.B < 0 || base.MT < 1 ||
+        base.MT > (base.binary ? kMaxMTBin : kMaxMT))
         return hipErrorInvalidValue;
     if ((mode == GF_MODE_INLINE || mode == GF_MODE_INLINE_LAT) &&
         (base.S != 1 || base.k > kInlineSrc || base.m > kInlineDst))
@@ -903,8 +943,10 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
     init_options();
     GfLaunch a = base;
     const long long vec_bytes = vec_ok ? (a.B & ~15LL) : 0;
+    g_launched.fetch_add((vec_bytes > 0) + (vec_bytes < a.B), std::memory_order_relaxed);
+    g_moved.fetch_add((long long)a.S * a.B * ((long long)a.rtiles * a.k + a.m), std::memory_order_relaxed);
     if (mode == GF_MODE_INLINE_LAT && vec_bytes == a.B && a.B <= g_opt[ECG_OPT_LAT_DWORD_BYTES].load() &&
-        a.k <= kLatMaxSrc && a.rtiles == 1) {
+        a.k <= kLatMaxSrc && a.rtiles == 1 && a.MT <= kMaxMT) {
         // small zero-copy call: 4 bytes per lane (gf_lat_dword_kernel)
         const long long gx = ((a.B >> 2) + kLatThreads - 1) / kLatThreads;
         Launcher l = a.binary ? pick_lat_dword_bin<true>(a.MT, a.k) : pick_lat_dword_bin<false>(a.MT, a.k);
@@ -931,7 +973,7 @@ hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t st
         if (gm == 2 && a.S % (8 * G) != 0) gm = 1;
         a.grid_map = (gm == 1 && gx % 8 == 0) ? 1 : (gm == 2) ? 2 : 0;
         a.map_group = (int)G;
-        const int nt = (int)g_opt[ECG_OPT_NT].load();
+        const int nt = a.MT > kMaxMT ? 3 : (int)g_opt[ECG_OPT_NT].load();  // wide tiles: built for the default only
         Launcher l = nullptr;
         switch (mode) {
             case GF_MODE_INLINE: l = pick_vec<GF_MODE_INLINE>(a, nt); break;

@@ -36,7 +36,9 @@ enum GfMode : int {
 
 constexpr int kInlineSrc = 128;
 constexpr int kInlineDst = 32;
-constexpr int kMaxMT = 8;       // output rows per row tile
+constexpr int kMaxMT = 8;       // output rows per row tile (GENERAL flavour)
+constexpr int kMaxMTBin = 16;   // BINARY flavour (one v_bitop3 per coefficient-dword): a composed product-code
+                                // call's 9-16 XOR rows read every input once (codes.cpp finish_plan)
 #ifndef ECG_TPB
 #define ECG_TPB 128
 #endif
@@ -124,6 +126,8 @@ int set_option(int opt, long long value);
 // Launch the region product over bytes [0, B) of every stripe.  `vec_ok` = every block pointer is
 // 16-byte aligned (the host checks); otherwise the byte path covers everything.  Returns a hipError_t.
 hipError_t launch_gf(const GfLaunch& base, int mode, bool vec_ok, hipStream_t stream, int* n_wg = nullptr);
+// Region-product kernels launch_gf has launched in this process, and the bytes they move as planned.
+void launch_traffic(long long* launches, long long* bytes);
 
 // Deterministic synthetic bytes: 8-byte word w = splitmix64(seed + (word_offset + w) * golden).
 hipError_t launch_fill_splitmix(void* dst, long long nbytes, unsigned long long seed,

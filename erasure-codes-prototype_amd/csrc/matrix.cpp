@@ -355,6 +355,66 @@ int plan_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const in
     return 0;
 }
 
+bool compose_chain(const std::vector<LinearOp>& ops, LinearOp& out) {
+    // dense ids over the blocks the chain names
+    std::vector<int> ids;
+    for (const LinearOp& op : ops) {
+        ids.insert(ids.end(), op.src_ids.begin(), op.src_ids.end());
+        ids.insert(ids.end(), op.dst_ids.begin(), op.dst_ids.end());
+    }
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    const int n = (int)ids.size();
+    auto at = [&](int id) { return (int)(std::lower_bound(ids.begin(), ids.end(), id) - ids.begin()); };
+    // content[b]: block b's bytes as a combination of the ORIGINAL contents (identity until written)
+    std::vector<std::vector<uint8_t>> content(n, std::vector<uint8_t>(n, 0));
+    for (int b = 0; b < n; b++) content[b][b] = 1;
+    std::vector<int> written;  // dense ids, first-write order
+    std::vector<char> is_written(n, 0);
+    std::vector<std::vector<uint8_t>> rows;
+    for (const LinearOp& op : ops) {
+        const int k = op.k_in(), m = op.m_out();
+        if (op.coef.size() != (size_t)k * m) return false;
+        rows.assign(m, std::vector<uint8_t>(n, 0));
+        for (int p = 0; p < m; p++)  // every row reads the values before this op's writes
+            for (int j = 0; j < k; j++) {
+                const int c = op.coef[(size_t)p * k + j];
+                if (!c) continue;
+                const std::vector<uint8_t>& src = content[at(op.src_ids[j])];
+                for (int b = 0; b < n; b++)
+                    if (src[b]) rows[p][b] ^= (uint8_t)gf::mul(c, src[b]);
+            }
+        for (int p = 0; p < m; p++) {
+            const int d = at(op.dst_ids[p]);
+            content[d] = std::move(rows[p]);
+            if (!is_written[d]) {
+                is_written[d] = 1;
+                written.push_back(d);
+            }
+        }
+    }
+    // one op over the original contents exists iff no written block's original bytes are read
+    std::vector<char> used(n, 0);
+    for (int w : written)
+        for (int b = 0; b < n; b++)
+            if (content[w][b]) {
+                if (is_written[b]) return false;
+                used[b] = 1;
+            }
+    LinearOp op;
+    for (int b = 0; b < n; b++)
+        if (used[b]) op.src_ids.push_back(ids[b]);
+    if (op.src_ids.empty()) return false;  // every output zero: leave such a chain as it is
+    op.coef.reserve(written.size() * op.src_ids.size());
+    for (int w : written) {
+        op.dst_ids.push_back(ids[w]);
+        for (int b = 0; b < n; b++)
+            if (used[b]) op.coef.push_back(content[w][b]);
+    }
+    out = std::move(op);
+    return true;
+}
+
 std::shared_ptr<const std::vector<LinearOp>> encode_plan_cached(int k, int m, const int* matrix) {
     struct Entry {
         std::vector<int> key;

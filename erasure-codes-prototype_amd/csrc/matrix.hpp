@@ -57,6 +57,14 @@ int plan_matrix_decode(int k, int m, const int* matrix, int row_k_ones, const in
 // An op is BINARY when every coefficient is 0 or 1 (pure XOR network).
 bool op_is_binary(const LinearOp& op);
 
+// A chain of ops run in order (each op reads what its sources hold after the ops before it) as ONE op over
+// the chain's original inputs: every block the chain writes, in first-write order, as its final linear
+// combination of the blocks it reads before they are written (exact: substitution over GF(2^8)).  Sources
+// are in ascending id order, columns that cancel to zero dropped.  false when no single op has the chain's
+// effect: a block whose original bytes a final value depends on is also written (the kernel would read it
+// while other workgroups write it), or every final value is zero.
+bool compose_chain(const std::vector<LinearOp>& ops, LinearOp& out);
+
 // plan_matrix_encode through a per-thread cache keyed by (k, m, matrix entries): the same plan object
 // for the same matrix, so per-stripe calls neither rebuild it nor copy it into a batch scope.
 std::shared_ptr<const std::vector<LinearOp>> encode_plan_cached(int k, int m, const int* matrix);

@@ -71,7 +71,7 @@ EXPORTS = [
     "ecg_jerasure_invert_matrix", "ecg_jerasure_matrix_multiply", "ecg_galois_region_xor",
     "ecg_jerasure_matrix_encode", "ecg_jerasure_matrix_decode", "ecg_jerasure_matrix_dotprod",
     "ecg_batch_begin", "ecg_batch_flush", "ecg_batch_end", "ecg_batch_defer_host", "ecg_batch_scratch",
-    "ecg_batch_last_stats",
+    "ecg_batch_last_stats", "ecg_traffic_counters",
     "ecg_dev_matrix_encode", "ecg_dev_matrix_decode", "ecg_matrix_apply_batch", "ecg_matrix_apply_batch_multi",
     "ecg_encode_batch",
     "ecg_decode_batch", "ecg_perform_addition_batch", "ecg_make_decode_matrix", "ecg_region_xor_batch", "ecg_encode_batch_host", "ecg_decode_batch_host",
@@ -166,6 +166,7 @@ def lib():
         "ecg_batch_end": ([], I),
         "ecg_batch_scratch": ([P, ctypes.c_size_t], I),
         "ecg_batch_last_stats": ([ctypes.POINTER(LL)] * 4, I),
+        "ecg_traffic_counters": ([ctypes.POINTER(LL)] * 2, I),
         "ecg_device_count": ([], I),
         "ecg_set_device": ([I], I),
         "ecg_free": ([P], None),
@@ -399,6 +400,14 @@ def batch_last_stats():
     v = [ctypes.c_longlong(0) for _ in range(4)]
     _check(lib().ecg_batch_last_stats(*[ctypes.byref(x) for x in v]), "batch_last_stats")
     return dict(zip(("recorded", "composed", "launches", "materialised"), (x.value for x in v)))
+
+
+def traffic_counters():
+    """Process-wide {launches, bytes}: region-product kernels launched so far and the bytes they move as planned
+    (S * B * (row tiles * k + m) per launch).  Differences over a region of calls give its executed traffic."""
+    v = [ctypes.c_longlong(0) for _ in range(2)]
+    _check(lib().ecg_traffic_counters(*[ctypes.byref(x) for x in v]), "traffic_counters")
+    return {"launches": v[0].value, "bytes": v[1].value}
 
 
 def dev_matrix_encode(k, m, matrix, data, coding, B, stream=None):

@@ -225,6 +225,12 @@ int ecg_batch_scratch(const void* ptr, size_t bytes);
 /* What this thread's last flush did: calls recorded, calls after scratch composition, launches (groups
  * x ops), scratch combinations written for real.  Any pointer may be NULL. */
 int ecg_batch_last_stats(long long* recorded, long long* composed, long long* launches, long long* materialised);
+/* Process-wide counters since the library loaded (diagnostics, every thread and device): region-product
+ * kernels launched, and the bytes they move as planned -- a launch of S stripes over B-byte blocks whose op
+ * reads k blocks and writes m, in row tiles that each read all k inputs, moves S * B * (tiles * k + m).  The
+ * difference over a region of calls is the traffic those calls executed (bench.py's executed bytes; PMC
+ * FETCH/WRITE counters agree where measured).  Either pointer may be NULL. */
+int ecg_traffic_counters(long long* launches, long long* bytes);
 /* Generic region product: out[dst_ids[p]] = XOR_j coef[p*k_in+j] * in[src_ids[j]] for S stripes,
  * in block b of stripe s at in_base + s*in_sstride + b*in_bstride (likewise out). */
 int ecg_matrix_apply_batch(int k_in, int m_out, const int* coef, const int* src_ids, const int* dst_ids,

@@ -22,16 +22,17 @@ LIB = os.path.join(ROOT, "erasure-codes-prototype_amd", "lib", "libecg.so")
 def test_every_flag_kernel_of_libecg_has_the_full_release_sequence():
     ks, flagged, bad = C.check(C.disassemble(LIB))
     # gf_lat_dword_kernel: 8 row tiles x 2 flavours x 6 input buckets x 2 (eager or not) = 192,
-    # gf_vec_kernel in INLINE_LAT mode (mode 3): 8 x 2 x 4 NT policies = 64
+    # gf_vec_kernel in INLINE_LAT mode (mode 3): 8 x 2 x 4 NT policies = 64, plus the wide BINARY tiles
+    # (9-16 rows, default NT policy only) = 8
     lat = [n for n in ks if "gf_lat_dword_kernel" in n]
     assert len(lat) == 192 and all(n in flagged for n in lat)
     inline_lat = re.compile(r"gf_vec_kernel<\d+, 3, \d+, (true|false)>")
     vec_lat = [n for n in ks if inline_lat.search(n)]
-    assert len(vec_lat) == 64 and all(n in flagged for n in vec_lat)
+    assert len(vec_lat) == 72 and all(n in flagged for n in vec_lat)
     # and the resident call worker (ECG_OPT_CALL_WORKER), which posts the same flags per call
     worker = [n for n in ks if "gf_call_worker_kernel" in n]
     assert len(worker) == 1 and worker[0] in flagged
-    assert len(flagged) == 257
+    assert len(flagged) == 265
     assert not bad, {n: p for n, p in list(bad.items())[:3]}
     # no other kernel writes the L2 back to the host (the batched kernels never post flags)
     assert all("gf_lat_dword_kernel" in n or inline_lat.search(n) or n in worker for n in flagged)

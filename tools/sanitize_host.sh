@@ -18,8 +18,9 @@ for f in matrix engine codes planning capi; do
   $HIPCC $CXX -fsanitize=address -fsanitize=undefined -fno-gpu-sanitize -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c $PKG/csrc/$f.cpp -o $OBJ/$f.o &
   pids+=($!)
 done
-$HIPCC $CXX --offload-arch=gfx950 --offload-host-only -fsanitize=address -fsanitize=undefined -fno-gpu-sanitize -c $PKG/csrc/gf_kernels.hip \
-  -o $OBJ/gf_kernels.o 2>/dev/null &
+( $HIPCC $CXX --offload-arch=gfx950 --offload-host-only -fsanitize=address -fsanitize=undefined -fno-gpu-sanitize \
+    -c $PKG/csrc/gf_kernels.hip -o $OBJ/gf_kernels.o 2>"$OBJ/gf_kernels.log" ||
+  { echo "sanitize_host.sh: host-only compile of gf_kernels.hip failed:" >&2; cat "$OBJ/gf_kernels.log" >&2; exit 1; } ) &
 pids+=($!)
 printf 'const char ecg_no_device_code[16] = {0};\n' > $OBJ/no_device_code.c
 gcc -c $OBJ/no_device_code.c -o $OBJ/no_device_code.o

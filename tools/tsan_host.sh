@@ -28,7 +28,9 @@ for f in matrix engine codes planning capi; do
   $CXX $FLAGS -std=c++17 $INC $EXTRA -x c++ -c $PKG/csrc/$f.cpp -o $OBJ/$f.o &
   pids+=($!)
 done
-$HIPCC $FLAGS -std=c++17 --offload-arch=gfx950 --offload-host-only -c $PKG/csrc/gf_kernels.hip -o $OBJ/gf_kernels.o 2>/dev/null &
+# its warnings (device-only attributes seen host-side) go to a log, printed if the compile fails
+( $HIPCC $FLAGS -std=c++17 --offload-arch=gfx950 --offload-host-only -c $PKG/csrc/gf_kernels.hip -o $OBJ/gf_kernels.o \
+    2>"$OBJ/gf_kernels.log" || { echo "tsan_host.sh: host-only compile of gf_kernels.hip failed:" >&2; cat "$OBJ/gf_kernels.log" >&2; exit 1; } ) &
 pids+=($!)
 $CXX $FLAGS -std=c++17 $INC -c tests/tsan/hip_stub.cpp -o $OBJ/hip_stub.o &
 pids+=($!)
