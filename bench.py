@@ -85,7 +85,7 @@ def parse():
     ap.add_argument("--workload", default="rs-encode-decode",
                     choices=["rs-encode-decode", "rs-decode-patterns", "lrc-repair", "lrc-repair-ring", "lrc-global-ring",
                              "pc-merge", "pc-merge-ring",
-                             "rs4m-waves", "rs-host", "rs-small-host"])
+                             "rs4m-waves", "rs-host", "rs-small-host", "families"])
     ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (default per workload)")
     ap.add_argument("--block-size", type=int, default=None)
     ap.add_argument("--chunk", type=int, default=None, help="lrc-repair-ring: stripes per transfer")
@@ -1010,6 +1010,8 @@ def replay_lib():
         L.ecg_replay_partial_repair_mt.restype = I
         L.ecg_replay_merge.argtypes = [P, P, I, I, P, LL, LL, I, I, I, I, P, P, P, I, P, P, P, P, P, LL, LL, P]
         L.ecg_replay_merge.restype = I
+        L.ecg_replay_calls.argtypes = [P, I, I, I, P, LL, LL, I, I, P, P, P, I, I, P, P]
+        L.ecg_replay_calls.restype = I
         L.ecg_replay_host_encode.argtypes = [I, I, P, P, P, I, I, I, I]
         L.ecg_replay_host_encode.restype = I
         _REPLAY = L
@@ -1390,6 +1392,304 @@ def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
 
 # ------------------------------------------------------------------------------- config 5
 
+# ------------------------------------------------------------------------------- every code family
+
+# (name, ECTYPE, coding parameters, the reference's class).  BASELINE's block size, working sets of >= 4 GiB
+# per class (far above the 256 MB Infinity Cache).  RS(20,4) / RS(30,4) are the stripes merging x = 2 / 3 RS(10,4)
+# stripes produces (merge.cpp:19-449; auxs.cpp:102-120 widens k to x k).
+FAMILIES = (
+    ("RS(12,4)", 0, dict(k=12, m=4), "rs.cpp:5-76"),
+    ("ERS(12,4|x=2,seri_num=1)", 1, dict(k=12, m=4, x=2, seri_num=1), "rs.cpp:282-305"),
+    ("Azure_LRC(12,2,2)", 2, dict(k=12, l=2, g=2), "lrc.cpp:576-873"),
+    ("Azure_LRC+1(12,3,2)", 3, dict(k=12, l=3, g=2), "lrc.cpp:881-1094"),
+    ("Optimal_LRC(12,2,2)", 4, dict(k=12, l=2, g=2), "lrc.cpp:1096-1307"),
+    ("Optimal_Cauchy_LRC(12,2,2)", 5, dict(k=12, l=2, g=2), "lrc.cpp:1309-1755"),
+    ("Uniform_Cauchy_LRC(12,2,2)", 6, dict(k=12, l=2, g=2), "lrc.cpp:2025-2310"),
+    ("PC(4,1,4,1)", 7, dict(k1=4, m1=1, k2=4, m2=1), "pc.cpp:5-551"),
+    ("HPC(4,1,4,1|x=2,seri_num=0)", 8, dict(k1=4, m1=1, k2=4, m2=1, x=2, seri_num=0), "pc.cpp:553-867"),
+    ("HVPC(4,1,4,1)", 9, dict(k1=4, m1=1, k2=4, m2=1), "pc.cpp:869-1267"),
+    ("RS(20,4)", 0, dict(k=20, m=4), "rs.cpp:5-76; merge.cpp:19-449"),
+    ("RS(30,4)", 0, dict(k=30, m=4), "rs.cpp:5-76; merge.cpp:19-449"),
+)
+FAMILY_OPS = ("encode", "repair1", "repair2", "decode2")
+FAMILY_WORKING_SET = 4 << 30
+
+
+def _call(kind, h, ins, outs, a=(), b=(), c=()):
+    """One ErasureCode call packed for ecg_replay_calls (loopback/replay.cpp)."""
+    return [kind, h, len(ins), *ins, len(outs), *outs, len(a), *a, len(b), *b, len(c), *c]
+
+
+def _repair_calls(plans, nb):
+    """The proxies' partial-decoding repair of one stripe (repair.cpp:192-330 -> handle_repair.cpp): per plan of
+    generate_repair_plan, one encode_partial_blocks_for_decoding per cluster's help blocks (handle 1 when the plan
+    is local / column, lrc.cpp:32-213, pc.cpp:290-324) into scratch slots, then perform_addition of the partials
+    into the failed blocks (written in place).  Returns (calls, scratch slots, algorithmic blocks)."""
+    calls, slot, alg = [], nb, 0
+    for pl in plans:
+        h, fails = (1 if pl.local_or_column else 0), list(pl.failure_idxs)
+        f = len(fails)
+        surv = [b for grp in pl.help_blocks for b in grp]
+        parts = []
+        for grp in pl.help_blocks:
+            outs = list(range(slot, slot + f))
+            slot += f
+            calls += _call(1, h, grp, outs, grp, surv, fails)
+            parts += outs
+        calls += _call(2, h, parts, fails, (len(parts), f))
+        alg += len(surv) + f
+    return calls, slot - nb, alg
+
+
+def _pack(progs):
+    prog, off = [], [0]
+    for p in progs:
+        prog += p
+        off.append(len(prog))
+    return torch.tensor(prog, dtype=torch.int32), torch.tensor(off, dtype=torch.int32)
+
+
+def _decode_deps(h, k, m, pat):
+    """Blocks the degraded-read decode of `pat` depends on (its result is linear in the survivors: survivor i is
+    read iff setting every other block to zero and i to random bytes gives nonzero output), on 64-byte host
+    blocks.  The algorithmic bytes of the decode are (these + the written blocks) * B."""
+    import numpy as np
+    n, B = k + m, 64
+    deps = []
+    rng = np.random.default_rng(len(pat) * 131 + pat[0])
+    for i in range(n):
+        if i in pat:
+            continue
+        st = [np.zeros(B, np.uint8) for _ in range(n)]
+        st[i][:] = rng.integers(1, 256, B, dtype=np.uint8)
+        er = list(pat) + [-1]
+        if h.decode(st[:k], st[k:], B, er, len(pat)) != 0:
+            raise RuntimeError(f"decode {pat} failed")
+        if any(st[j].any() for j in pat):
+            deps.append(i)
+    return deps
+
+
+def families(a, r):
+    """Every ErasureCode class of the reference (ec_factory, metadata.cpp:48-77) through the facade, as the proxies
+    call it, per stripe, in batch scopes (scratch partials declared, so a repair's partials compose away): four
+    operations per class over >= 4 GiB of 1 MiB-block stripes --
+      encode   ErasureCode::encode of every stripe (proxy.cpp:346);
+      repair1  single-block repair of block s mod n with the class's own generate_repair_plan and partition
+               (repair.cpp:22-26): a partial decode per cluster's help blocks + perform_addition;
+      repair2  two-block repair (blocks i, i + n/2 of stripe i mod n), same path (run_client.cpp:62-122);
+      decode2  degraded-read decode of the same two blocks (ErasureCode::decode, proxy.cpp:666).
+    Each row: HIP-event time per batch, algorithmic bytes (encode (k+m) B; repairs (survivors + failed) B per
+    plan; decode (blocks the result depends on + written) B) and their fraction of 8 TB/s, the executed bytes
+    the library's launches moved (ecg_traffic_counters) over the algorithmic, launches per batch, the launch
+    range of the timed batches (tools/families_profile.py maps it to the rocprofv3 kernel trace), and every
+    stripe verified: repairs and decodes rebuild poisoned blocks equal to the encoded ones.  --forms filters
+    classes by name prefix.  Rank 0 at N = 1 adds a CPU leg per row: the oracle's class restatement of the same
+    calls on sampled stripes, timed, and its outputs compared with the GPU's."""
+    import ctypes
+    B = a.block_size or (1 << 20)
+    steps, warmup = a.steps, a.warmup
+    want = a.forms.split(",") if a.forms else None
+    rp = replay_lib()
+    out = {"workload": "families: encode, single- and two-block repair (partial decoding, generate_repair_plan help "
+                       "blocks), two-erasure degraded-read decode of every ErasureCode class, 1 MiB blocks",
+           "n_gpus": r.world, "block_size": B, "steps": steps, "warmup": warmup, "dtype": "u8",
+           "data": "synthetic (splitmix64 bytes generated on device)", "classes": {}}
+    for name, t, params, anchor in FAMILIES:
+        if want and not any(name.startswith(w) for w in want):
+            continue
+        torch.cuda.empty_cache()
+        cp, cpl = ecg.CodingParameters(**params), ecg.CodingParameters(**params, local_or_column=True)
+        hG, hL = ecg.ec_factory(t, cp), ecg.ec_factory(t, cpl)
+        hG.init_coding_parameters(cp)
+        hL.init_coding_parameters(cpl)
+        k, m = hG.k, hG.m
+        n = k + m
+        hG.generate_partition()
+        hL.partition_plan = hG.partition_plan
+        S = a.stripes or -(-FAMILY_WORKING_SET // (n * B))
+        S = -(-S // n) * n  # whole rounds of the n single-block patterns
+        pats2 = [sorted({i, (i + n // 2) % n}) for i in range(n)]
+        pats2 = [p for p in pats2 if hG.check_if_decodable(p)]
+        progs = {"encode": ([_call(0, 0, range(k), range(k, n))], [k + m], None)}
+        for op, pats in (("repair1", [[f] for f in range(n)]), ("repair2", pats2)):
+            cl, algs, nscr = [], [], 0
+            for p in pats:
+                ok, plans = hG.generate_repair_plan(p)
+                if not ok:
+                    raise RuntimeError(f"{name}: no repair plan for {p}")
+                c, ns, al = _repair_calls(plans, n)
+                cl.append(c)
+                algs.append(al)
+                nscr = max(nscr, ns)
+            progs[op] = (cl, algs, pats)
+        progs["decode2"] = ([_call(3, 0, range(k), range(k, n), list(p) + [-1], [len(p)]) for p in pats2],
+                            [len(_decode_deps(hG, k, m, p)) + len(p) for p in pats2], pats2)
+        stripes = torch.empty((S, n, B), dtype=torch.uint8, device="cuda")
+        ecg.fill_random(stripes, 0xEC0DE, word_offset=D.data_word_offset(r.rank * S, n, B))
+        scratch = torch.empty((S, max(nscr, 1), B), dtype=torch.uint8, device="cuda")
+        handles = (ctypes.c_void_p * 2)(hG._h, hL._h)
+        truth = None
+        cls = {"reference": anchor, "k": k, "m": m, "stripes_per_gpu": S,
+               "working_set_GiB": round(S * n * B / 2 ** 30, 2), "ops": {}}
+        for op in FAMILY_OPS:
+            cl, algs, pats = progs[op]
+            prog, off = _pack(cl)
+            npat = len(cl)
+            pat_of = torch.arange(S, dtype=torch.int32) % npat
+            alg = sum(algs[s % npat] for s in range(S)) * B
+            failed = None
+            if pats is not None:
+                failed = [(s, b) for s in range(S) for b in pats[s % npat]]
+                fs = torch.tensor([x[0] for x in failed], device="cuda")
+                fb = torch.tensor([x[1] for x in failed], device="cuda")
+
+            def poison():
+                if failed is not None:
+                    stripes[fs, fb] = 0xA5
+
+            def fn(ev=None):
+                if ev:
+                    ev[0].record()
+                st = torch.cuda.current_stream().cuda_stream
+                rc = rp.ecg_replay_calls(handles, 2, 64 if n * B * 64 <= (2 << 30) else 32, 1, stripes.data_ptr(),
+                                         stripes.stride(0), stripes.stride(1), B, S, pat_of.data_ptr(), prog.data_ptr(),
+                                         off.data_ptr(), n, scratch.shape[1], scratch.data_ptr(), st)
+                if rc != 0:
+                    raise ecg.EcgError(rc, f"ecg_replay_calls({name}, {op})")
+                if ev:
+                    ev[1].record()
+
+            poison()
+            for _ in range(warmup):
+                fn()
+            torch.cuda.synchronize()
+            if op == "encode":
+                truth = stripes.clone()
+            c0 = ecg.traffic_counters()
+            elapsed, evs = timed_loop(r, steps, fn)
+            c1 = ecg.traffic_counters()
+            tt = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+            # the check: a pass that starts from poisoned blocks rebuilds every one of them, nothing else changes
+            poison()
+            fn()
+            torch.cuda.synchronize()
+            verified = bool(torch.equal(stripes, truth))
+            executed = (c1["bytes"] - c0["bytes"]) / steps
+            row = {"ms_per_batch": round(tt * 1e3, 3), "algorithmic_bytes_per_batch": alg,
+                   "algorithmic_GBps": round(alg / tt / 1e9, 1), "frac": round(alg / tt / 1e9 / HBM_PEAK_GBS, 4),
+                   "executed_bytes_per_batch": int(executed), "executed_over_algorithmic": round(executed / alg, 4),
+                   "executed_frac": round(executed / tt / 1e9 / HBM_PEAK_GBS, 4),
+                   "launches_per_batch": (c1["launches"] - c0["launches"]) / steps,
+                   "calls_per_batch": sum(_ncalls(cl[s % npat]) for s in range(S)),
+                   "launch_range": [c0["launches"], c1["launches"]], "verified": verified,
+                   "ops_per_s": round(r.world * S * steps / elapsed, 1)}
+            if pats is not None:
+                row["patterns"] = len(pats)
+                row["algorithmic_blocks_per_pattern"] = algs
+            cls["ops"][op] = row
+        if r.world == 1 and r.rank == 0 and not a.no_cpu_baseline:
+            try:
+                cls["cpu_check"] = families_cpu_leg(t, params, k, m, B, progs, stripes, truth, n, scratch.shape[1])
+            except Exception as e:  # noqa: BLE001 -- reported beside the GPU rows
+                cls["cpu_check"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+        out["classes"][name] = cls
+        del stripes, scratch, truth
+    fr = [(c, o, v["frac"]) for c, cv in out["classes"].items() for o, v in cv["ops"].items()]
+    out["min_frac"] = min(fr, key=lambda x: x[2]) if fr else None
+    out["all_verified"] = all(v["verified"] for cv in out["classes"].values() for v in cv["ops"].values())
+    out["build"] = build_provenance()
+    return out
+
+
+def _ncalls(packed):
+    """Calls in one packed call list."""
+    i = c = 0
+    while i < len(packed):
+        n_in = packed[i + 2]
+        n_out = packed[i + 3 + n_in]
+        q = i + 4 + n_in + n_out
+        n_a = packed[q]
+        n_b = packed[q + 1 + n_a]
+        n_c = packed[q + 2 + n_a + n_b]
+        i = q + 3 + n_a + n_b + n_c
+        c += 1
+    return c
+
+
+def families_cpu_leg(t, params, k, m, B, progs, stripes, truth, n, nscr):
+    """cpu_baseline leg of the families workload: the oracle's restatement of the reference classes
+    (oracle/ec_ref.py, region products on its SIMD split-table kernels) runs the same packed calls on sampled
+    stripes, one thread, timed; its outputs are the checker of the GPU's stripes (encode: the GPU's parities;
+    repairs / decodes: the blocks rebuilt from poisoned ones)."""
+    import numpy as np
+    from oracle import ec_ref as E
+    from oracle import ref as J
+    J.build()
+    cp, cpl = E.CodingParameters(**params), E.CodingParameters(**params, local_or_column=True)
+    oG, oL = E.ec_factory(t, cp), E.ec_factory(t, cpl)
+    oG.init_coding_parameters(cp)
+    oL.init_coding_parameters(cpl)
+    oL.local_or_column = True
+    hs = (oG, oL)
+    res = {"kind": "port", "cores": 1, "threads_used": 1}
+    scalar = J.jerasure_matrix_encode
+    J.jerasure_matrix_encode = J.jerasure_matrix_encode_simd  # same semantics, the SIMD region kernels
+    try:
+        for op in FAMILY_OPS:
+            cl, algs, pats = progs[op]
+            npat = len(cl)
+            sample = sorted({0, min(k, npat - 1), npat - 1}) if pats is not None else [0]
+            t_total, alg, ok = 0.0, 0, True
+            for s in sample:
+                blocks = [x.copy() for x in truth[s].cpu().numpy()]
+                if pats is not None:
+                    for b in pats[s % npat]:
+                        blocks[b][:] = 0xA5
+                else:
+                    for b in range(k, n):
+                        blocks[b][:] = 0
+                scr = [np.zeros(B, np.uint8) for _ in range(nscr)]
+                get = lambda i: blocks[i] if i < n else scr[i - n]  # noqa: E731
+                packed = cl[s % npat]
+                t0 = time.perf_counter()
+                i = 0
+                while i < len(packed):
+                    kind, h, n_in = packed[i], packed[i + 1], packed[i + 2]
+                    ins = packed[i + 3:i + 3 + n_in]
+                    n_out = packed[i + 3 + n_in]
+                    outs = packed[i + 4 + n_in:i + 4 + n_in + n_out]
+                    q = i + 4 + n_in + n_out
+                    na = packed[q]
+                    av = packed[q + 1:q + 1 + na]
+                    nb_ = packed[q + 1 + na]
+                    bv = packed[q + 2 + na:q + 2 + na + nb_]
+                    nc = packed[q + 2 + na + nb_]
+                    cv = packed[q + 3 + na + nb_:q + 3 + na + nb_ + nc]
+                    i = q + 3 + na + nb_ + nc
+                    o = hs[h]
+                    I, O = [get(x) for x in ins], [get(x) for x in outs]
+                    if kind == 0:
+                        o.encode(I, O, B)
+                    elif kind == 1:
+                        o.encode_partial_blocks_for_decoding(I, O, B, list(av), list(bv), list(cv))
+                    elif kind == 2:
+                        o.perform_addition(I, O, B, av[0], av[1])
+                    elif kind == 3:
+                        if o.decode(I, O, B, list(av), bv[0]) != 0:
+                            ok = False
+                t_total += time.perf_counter() - t0
+                alg += algs[s % npat] * B
+                ok &= all(np.array_equal(blocks[b], truth[s, b].cpu().numpy()) for b in range(n))
+            res[op] = {"GBps": round(alg / t_total / 1e9, 3), "stripes": len(sample), "seconds": round(t_total, 3),
+                       "matches_gpu": bool(ok)}
+    finally:
+        J.jerasure_matrix_encode = scalar
+    res["sample"] = ("the same ErasureCode calls on 1-3 stripes per operation through oracle/ec_ref.py (Python "
+                     "class restatement over the C oracle's SIMD region multiply), one thread")
+    return res
+
+
 def encode_waves(k, m, M, B, first, last, W, seed=0xEC0DE, on_wave=None):
     """Encode global stripes [first, last) of the synthetic RS(k, m) batch in HBM-resident waves of at most
     W stripes ([W][k+m][B] in one buffer).  Each wave's data is regenerated on device from the stripes'
@@ -1642,7 +1942,7 @@ def main():
     fn = {"rs-encode-decode": rs_encode_decode, "rs-decode-patterns": rs_decode_patterns, "lrc-repair": lrc_repair,
           "lrc-repair-ring": lrc_repair_ring, "lrc-global-ring": lrc_global_ring, "pc-merge": pc_merge,
           "pc-merge-ring": pc_merge_ring,
-          "rs4m-waves": rs4m_waves, "rs-host": rs_host, "rs-small-host": rs_small_host}[a.workload]
+          "rs4m-waves": rs4m_waves, "rs-host": rs_host, "rs-small-host": rs_small_host, "families": families}[a.workload]
     line = fn(a, r)
     if r.rank == 0:
         print(json.dumps(line), flush=True)

@@ -161,6 +161,98 @@ int ecg_replay_merge(ecg_ec* main_ec, ecg_ec* help_ec, int form, int scope_merge
     return 0;
 }
 
+// Any per-stripe sequence of ErasureCode calls, for bench.py's `families` workload (every code class the
+// reference builds, ec_factory metadata.cpp:48-77: encode, repair through generate_repair_plan's help blocks,
+// degraded-read decode).  Stripe s (of S) runs the calls of pattern pattern_of[s]; pattern p's calls are
+// prog[off[p] .. off[p + 1]), each call packed as
+//   [kind, handle, n_in, in ids.., n_out, out ids.., n_a, a.., n_b, b.., n_c, c..]
+// kind 0 encode(in = k data blocks, out = m coding blocks)                              erasure_code.h:86
+//      1 encode_partial_blocks_for_decoding(in, out; a = local_survivor_idxs, b = survivor_idxs,
+//        c = failure_idxs)                                                              handle_repair.cpp:249,566
+//      2 perform_addition(in = partials, out; a = [block_num, parity_num])              handle_repair.cpp:375
+//      3 decode(in = k data blocks, out = m coding blocks; a = erasures incl. the -1 (copied per call: the LRC
+//        local path writes into it, lrc.cpp:35-38), b = [failed_num])                   proxy.cpp:666
+//      4 encode_partial_blocks_for_encoding(in, out; a = data_idxs, b = parity_idxs)    handle_merge.cpp:453
+// Block ids below nb are the stripe's blocks (base + s * sstride + id * bstride); ids nb .. nb + nscr - 1 are
+// the stripe's scratch slots (scratch + (s * nscr + id - nb) * B), e.g. the partials a repair adds.  Calls run
+// in batch scopes of scope_stripes stripes (0 = every call on its own), with the scratch slots of the scope
+// declared ecg_batch_scratch when use_scratch (the partials of a repair then compose away).  Every handle is
+// set to device memory on `stream`.  Returns 0 or the first negative status.
+int ecg_replay_calls(ecg_ec** handles, int n_handles, int scope_stripes, int use_scratch, char* base, long long sstride,
+                     long long bstride, int B, int S, const int* pattern_of, const int* prog, const int* off, int nb,
+                     int nscr, char* scratch, void* stream) {
+    if (!handles || n_handles < 1 || B <= 0 || S < 0 || nb < 1 || nscr < 0 || scope_stripes < 0 || !prog || !off)
+        return ECG_EINVAL;
+    for (int h = 0; h < n_handles; h++)
+        if (int rc = ecg_ec_set_memory(handles[h], ECG_MEM_DEVICE, stream)) return rc;
+    std::vector<char*> in, out;
+    std::vector<int> er;
+    auto blk = [&](int s, int id) -> char* {
+        return id < nb ? base + (long long)s * sstride + (long long)id * bstride
+                       : scratch + ((long long)s * nscr + (id - nb)) * B;
+    };
+    auto stripe = [&](int s) -> int {
+        const int p = pattern_of ? pattern_of[s] : 0;
+        for (int i = off[p]; i < off[p + 1];) {
+            const int* c = prog + i;
+            const int kind = c[0], h = c[1];
+            if (h < 0 || h >= n_handles) return ECG_EINVAL;
+            ecg_ec* ec = handles[h];
+            const int n_in = c[2];
+            const int* ids_in = c + 3;
+            const int n_out = c[3 + n_in];
+            const int* ids_out = c + 4 + n_in;
+            const int* q = ids_out + n_out;
+            const int n_a = q[0];
+            const int* a = q + 1;
+            const int n_b = a[n_a];
+            const int* b = a + n_a + 1;
+            const int n_c = b[n_b];
+            const int* cc = b + n_b + 1;
+            i += 4 + n_in + n_out + 3 + n_a + n_b + n_c;
+            in.resize(n_in);
+            out.resize(n_out);
+            for (int j = 0; j < n_in; j++) in[j] = blk(s, ids_in[j]);
+            for (int j = 0; j < n_out; j++) out[j] = blk(s, ids_out[j]);
+            int rc;
+            switch (kind) {
+                case 0: rc = ecg_ec_encode(ec, in.data(), out.data(), B); break;
+                case 1:
+                    rc = ecg_ec_encode_partial_blocks_for_decoding(ec, in.data(), out.data(), B, a, n_a, b, n_b, cc, n_c);
+                    break;
+                case 2: rc = n_a == 2 ? ecg_ec_perform_addition(ec, in.data(), out.data(), B, a[0], a[1]) : ECG_EINVAL; break;
+                case 3:
+                    er.assign(a, a + n_a);
+                    rc = n_b == 1 ? ecg_ec_decode(ec, in.data(), out.data(), B, er.data(), b[0]) : ECG_EINVAL;
+                    break;
+                case 4: rc = ecg_ec_encode_partial_blocks_for_encoding(ec, in.data(), out.data(), B, a, n_a, b, n_b); break;
+                default: rc = ECG_EINVAL;
+            }
+            if (rc) return rc;
+        }
+        return 0;
+    };
+    int rc = 0;
+    if (scope_stripes == 0) {
+        for (int s = 0; s < S && !rc; s++) rc = stripe(s);
+        return rc;
+    }
+    for (int c0 = 0; c0 < S; c0 += scope_stripes) {
+        const int c1 = c0 + scope_stripes < S ? c0 + scope_stripes : S;
+        if ((rc = ecg_batch_begin())) return rc;
+        if (use_scratch && nscr > 0 &&
+            (rc = ecg_batch_scratch(scratch + (long long)c0 * nscr * B, (size_t)(c1 - c0) * nscr * B))) {
+            ecg_batch_end();
+            return rc;
+        }
+        for (int s = c0; s < c1 && !rc; s++) rc = stripe(s);
+        const int re = ecg_batch_end();
+        if (rc) return rc;
+        if (re) return re;
+    }
+    return 0;
+}
+
 // Config 1's per-stripe host calls (proxy.cpp:312-349: one jerasure_matrix_encode per stripe on the
 // proxy's host buffers): data [S][k][B], coding [S][m][B] in host memory.  mode 0: one synchronous call
 // per stripe; mode 1: the same calls inside batch scopes of `per_scope` stripes with host deferral on
