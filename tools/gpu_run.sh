@@ -17,6 +17,8 @@
 #   wprof      rocprofv3 kernel stats of each non-default workload
 #   w:<name>   one workload line                                                  -> bench_<name>.log
 #   wp:<name>  rocprofv3 kernel stats of one workload
+#   families   bench.py --workload families (every code class: encode, repairs, decode)   -> families.log
+#   famprof    rocprofv3 kernel trace of the families workload + tools/families_profile.py -> families_profile.json
 #   w34prof    rocprofv3 kernel traces of each form the line's config3 / config4 objects time (one run per
 #              form) -> workload_profile.json (tools/workload_profile.py; copy it to profiles/ for bench.py)
 #   ceiling    tools/movement_ceiling: the product kernel's own access path with the multiply removed, and its
@@ -100,6 +102,11 @@ for step in "$@"; do
     w:*) w=${step#w:}; run "bench $w" 500 "$O/bench_$w.log" python bench.py --workload $w --no-cpu-baseline
          tail -1 "$O/bench_$w.log" | cut -c1-600 ;;
     wp:*) w=${step#wp:}; prof "wprof/$w" "wprof_$w.log" --workload $w --no-cpu-baseline ;;
+    families) run families 900 "$O/families.log" python bench.py --workload families --steps ${FSTEPS:-5} --warmup 2 \
+                ${FARGS:-}; tail -c 600 "$O/families.log"; echo ;;
+    famprof) prof famprof famprof.log --workload families --steps ${FSTEPS:-5} --warmup 2 --no-cpu-baseline ${FARGS:-}
+             python tools/families_profile.py "$O/famprof/run_kernel_trace.csv" "$O/famprof.log" \
+               "$O/families_profile.json" > "$O/families_profile.log" 2>&1 && echo "families_profile ok" || exit 1 ;;
     w34prof) C3="fused reference_sequence_scope_scratch reference_sequence_per_call reference_sequence_per_call_threads8"
              C4="rows fused reference_sequence_scope_scratch reference_sequence_per_call"
              spec=""
