@@ -260,14 +260,41 @@ def test_facade_decode_vs_oracle(ecg, oracle, torch_cuda, name, t, params):
         for i in pat:
             A[i][:] = 0
             Bb[i][:] = 0
-        if t in (2, 3, 4, 5, 6):  # LRC global decode: -1-terminated list
-            ea, eb = pat + [-1], pat + [-1]
-        else:
-            ea, eb = pat + [-1], pat + [-1]
-        ra = o.decode(A[:o.k], A[o.k:], B, ea, len(pat))
-        rb = p.decode(Bb[:o.k], Bb[o.k:], B, eb, len(pat))
+        ra = o.decode(A[:o.k], A[o.k:], B, pat + [-1], len(pat))  # -1-terminated (LRCs: the global path)
+        rb = p.decode(Bb[:o.k], Bb[o.k:], B, pat + [-1], len(pat))
         assert (ra == 0) == (rb == 0), (pat, ra, rb)
         assert same(A, Bb), pat
+    if t in (2, 3, 4, 5, 6):
+        _lrc_local_decodes(E, t, params, stripe, B, rng)
+
+
+def _lrc_local_decodes(E, t, params, stripe, B, rng):
+    """The LRC local path of ErasureCode::decode (lrc.cpp:32-42,58-72), as main_repair calls it without partial
+    decoding (handle_repair.cpp:377-384): local_or_column set, the group's blocks in group space (data_ptrs:
+    the group_size members, coding_ptrs: its local parity), erasures = [index in the group, group_id] with
+    failed_num = 1 -- group_id rides in erasures[failed_num] (handle_repair.cpp:380-381) and comes back as -1.
+    Every position of every group (the local parity included), plus random positions with garbage in the
+    lost block; status and every byte against the oracle.  (The Cauchy LRCs' group rows are not all ones, so
+    some of their lost data blocks come back wrong in both -- Appendix B.1, test_cauchy_local_decode_quirk.)"""
+    o, p = _pair(t, params, local=True)
+    k, g, l = o.k, o.g, o.l
+    for gid in range(l):
+        gs, mn = o.get_group_size(gid)
+        members = (list(range(mn, mn + gs - g)) + list(range(k, k + g))) if t == 5 else list(range(mn, mn + gs))
+        group = [stripe[b] for b in members] + [stripe[k + g + gid]]
+        for lost in list(range(gs + 1)) + [rng.randrange(gs + 1) for _ in range(2)]:
+            A = [x.copy() for x in group]
+            Bq = [x.copy() for x in group]
+            A[lost][:] = 0xD1
+            Bq[lost][:] = 0xD1
+            ea, eb = [lost, gid], [lost, gid]
+            ra = o.decode(A[:gs], A[gs:], B, ea, 1)
+            rb = p.decode(Bq[:gs], Bq[gs:], B, eb, 1)
+            assert (ra == 0) == (rb == 0), (t, gid, lost, ra, rb)
+            assert eb == [lost, -1], eb  # lrc.cpp:36: the group id slot is overwritten with -1
+            assert same(A, Bq), (t, gid, lost)
+            if t not in (5, 6):  # all-ones group rows: the local decode rebuilds the lost block
+                assert np.array_equal(Bq[lost], group[lost]), (t, gid, lost)
 
 
 @pytest.mark.parametrize("name,t,params", CODES)
