@@ -1582,7 +1582,7 @@ def family_rows(a, r, rp, name, t, params, anchor, B, steps, warmup):
             if ev:
                 ev[0].record()
             st = torch.cuda.current_stream().cuda_stream
-            rc = rp.ecg_replay_calls(handles, 2, 64 if n * B * 64 <= (2 << 30) else 32, 1, stripes.data_ptr(),
+            rc = rp.ecg_replay_calls(handles, 2, S, 1, stripes.data_ptr(),  # one scope per batch
                                      stripes.stride(0), stripes.stride(1), B, S, pat_of.data_ptr(), prog.data_ptr(),
                                      off.data_ptr(), n, scratch.shape[1], scratch.data_ptr(), st)
             if rc != 0:

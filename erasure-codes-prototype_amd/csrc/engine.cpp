@@ -1275,9 +1275,13 @@ namespace {
 
 // Plan classes of a flush: calls with equal plans (by content), block size, stream and device share a
 // class.  Recording shares the plan pointer between consecutive equal calls, so most lookups hit the
-// pointer cache; composed calls are interned by content.
+// pointer cache; composed calls are interned by content.  Single-op plans of one shape (k_in, m_out) share a
+// class whatever their coefficients: the per-stripe repairs of a batch (a pattern per stripe, each composing
+// to its own matrix) then go out as ONE multi-program pointer-table launch per scope instead of a launch per
+// pattern (families workload: RS(12,4) repairs 16 patterns x 4 scopes -> 4 launches).
 class PlanClasses {
 public:
+    int plan_of_last() const { return last_plan_; }
     int of(const DeferredCall& c) {
         auto pk = by_ptr_.find(c.ops.get());
         int plan;
@@ -1305,7 +1309,15 @@ public:
             }
             by_ptr_[c.ops.get()] = plan;
         }
-        const auto key = std::make_tuple(plan, c.eng, c.st, c.B);
+        last_plan_ = plan;
+        int cls_plan = plan;
+        if (c.ops->size() == 1 && (*c.ops)[0].k_in() > 0) {
+            const auto sk = std::make_pair((*c.ops)[0].k_in(), (*c.ops)[0].m_out());
+            auto si = shapes_.find(sk);
+            if (si == shapes_.end()) si = shapes_.emplace(sk, (int)shapes_.size()).first;
+            cls_plan = -1 - si->second;
+        }
+        const auto key = std::make_tuple(cls_plan, c.eng, c.st, c.B);
         auto it = cls_.find(key);
         if (it != cls_.end()) return it->second;
         const int id = (int)cls_.size();
@@ -1317,7 +1329,9 @@ private:
     std::unordered_map<const void*, int> by_ptr_;
     std::unordered_map<size_t, std::vector<int>> by_hash_;
     std::vector<std::shared_ptr<const std::vector<LinearOp>>> plans_;
+    std::map<std::pair<int, int>, int> shapes_;
     std::map<std::tuple<int, Engine*, hipStream_t, long long>, int> cls_;
+    int last_plan_ = -1;
 };
 
 }  // namespace
@@ -1353,13 +1367,18 @@ int batch_flush() {
     if (!d.scratch.empty()) q = compose_scratch(std::move(q), d.scratch, /*scope_end=*/!d.active, &st.materialised);
     st.composed = (long long)q.size();
     std::vector<std::vector<size_t>> groups;
+    std::vector<int> plan_id;  // per call: its plan (by content); empty on the fast path (one plan)
     if (d.scratch.empty() && one_disjoint_strided_group(q)) {  // the per-stripe loop over one batch
         groups.emplace_back(q.size());
         std::iota(groups[0].begin(), groups[0].end(), (size_t)0);
     } else {
         PlanClasses classes;
         std::vector<int> cls(q.size());
-        for (size_t c = 0; c < q.size(); c++) cls[c] = classes.of(q[c]);
+        plan_id.resize(q.size());
+        for (size_t c = 0; c < q.size(); c++) {
+            cls[c] = classes.of(q[c]);
+            plan_id[c] = classes.plan_of_last();
+        }
         auto reads = [&](size_t c, auto&& f) {
             for (const LinearOp& op : *q[c].ops)
                 for (int id : op.src_ids) f(q[c].blocks[id]);
@@ -1423,6 +1442,17 @@ int batch_flush() {
         std::vector<const uint8_t* const*> calls;
         calls.reserve(G.size());
         for (size_t c : G) calls.push_back(q[c].blocks.data());
+        bool mixed = false;  // single-op plans of one shape, several matrices (PlanClasses)
+        if (!plan_id.empty())
+            for (size_t c : G) mixed |= plan_id[c] != plan_id[G[0]];
+        if (mixed) {
+            std::vector<const LinearOp*> per_call;
+            per_call.reserve(G.size());
+            for (size_t c : G) per_call.push_back(&(*q[c].ops)[0]);
+            rc = eng->run_ptr_batch_multi(per_call, calls, c0.B, c0.st);
+            st.launches++;
+            continue;
+        }
         for (const LinearOp& op : *c0.ops) {
             if (op.k_in() == 0) {  // composed row of zeros: the library writes zero bytes
                 for (size_t c : G) {

@@ -1609,8 +1609,8 @@ def _repair_sequence(ec, st, plan, partials, out, B):
 
 def test_batch_scope_interleaved_plans_group(ecg, torch_cuda):
     """Per-stripe repairs interleave three plans per stripe and a different erasure per stripe; the scope
-    still launches one launch per distinct plan (calls reordered where nothing orders them), and the
-    bytes are the sequential ones."""
+    still launches one launch per distinct plan SHAPE (single-op plans of one shape share a multi-program
+    pointer-table launch; calls reordered where nothing orders them), and the bytes are the sequential ones."""
     torch = torch_cuda
     S, B = 56, 64 * 1024
     ec, st, plan = _azure_repair_state(ecg, torch, S, B, 0x5C0)
@@ -1624,10 +1624,10 @@ def test_batch_scope_interleaved_plans_group(ecg, torch_cuda):
     want = st[idx, torch.tensor([p[0] for p in plan], device="cuda")]
     assert torch.equal(out, want)
     assert stats["recorded"] == 3 * S and stats["composed"] == 3 * S
-    # one launch per distinct plan (partial plans are equal when their coefficient rows are: Azure's local
-    # rows are all ones, so every helper and main partial shares one plan), + the perform_addition plan
-    plans = {tuple(ec.partial_decoding_matrix(sets[i], surv, [e])) for e, surv, sets in plan for i in range(2)}
-    assert stats["launches"] == len(plans) + 1, (stats, plans)
+    # one launch per distinct (k_in, m_out) of the partial plans -- whatever their matrices -- + the
+    # perform_addition plan, which reads the partials
+    shapes = {(len(sets[i]), 1) for e, surv, sets in plan for i in range(2)}
+    assert stats["launches"] == len(shapes) + 1, (stats, shapes)
 
 
 def test_batch_scope_scratch_composes_partials(ecg, oracle, torch_cuda):
