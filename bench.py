@@ -109,6 +109,8 @@ def parse():
                     help="default workload: skip the config3 / config4 sub-objects (LRC repair, PC merge on one GPU)")
     ap.add_argument("--configs34-stripes", type=int, default=None,
                     help="default workload: stripes (config 3) / merges (config 4) per GPU (default 4096 / 512)")
+    ap.add_argument("--working-set-gib", type=float, default=4.0,
+                    help="families: stripes per class so the stripes take at least this many GiB (default 4)")
     ap.add_argument("--ring-scale", type=float, default=1.0,
                     help="default workload: scale the cross-GPU objects' stripe / merge counts (rehearsals of many "
                          "ranks on one GPU)")
@@ -1412,7 +1414,6 @@ FAMILIES = (
     ("RS(30,4)", 0, dict(k=30, m=4), "rs.cpp:5-76; merge.cpp:19-449"),
 )
 FAMILY_OPS = ("encode", "repair1", "repair2", "decode2")
-FAMILY_WORKING_SET = 4 << 30
 
 
 def _call(kind, h, ins, outs, a=(), b=(), c=()):
@@ -1528,7 +1529,7 @@ def family_rows(a, r, rp, name, t, params, anchor, B, steps, warmup):
     hP = ecg.ec_factory(t, cp)
     hP.init_coding_parameters(cp)
     hP.generate_partition()
-    S = a.stripes or -(-FAMILY_WORKING_SET // (n * B))
+    S = a.stripes or -(-int(a.working_set_gib * 2 ** 30) // (n * B))
     S = -(-S // n) * n  # whole rounds of the n single-block patterns
     pats2 = [sorted({i, (i + n // 2) % n}) for i in range(n)]
     pats2 = [p for p in pats2 if hP.check_if_decodable(p)]

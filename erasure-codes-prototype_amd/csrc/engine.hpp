@@ -373,18 +373,22 @@ private:
 
 // Grouping of the flush (pure host logic, no HIP; fuzzed against a quadratic legality check in
 // tests/sanitize/host_fuzz.cpp).  Calls [0, n) in program order; key(c) >= 0 names the call's plan
-// class (same plan, block size, stream, device).  Each call joins the LATEST group of its key if that
-// group comes after every group holding an earlier call it depends on (one that writes a block it reads
-// or writes, or reads a block it writes); otherwise it opens a new group at the end.  Launching the
-// groups in index order, each group's calls in one launch, therefore respects every dependence of the
-// program order (two dependent calls always sit in groups i < j), and independent calls of one plan --
-// the reference's per-stripe loop, even with several plans interleaved per stripe -- share a launch.
+// class (same plan or single-op shape, block size, stream, device).  Each call joins the EARLIEST group of
+// its key that comes after every group holding an earlier call it depends on (one that writes a block it
+// reads or writes, or reads a block it writes); if there is none it opens a new group at the end.
+// Launching the groups in index order, each group's calls in one launch, therefore respects every
+// dependence of the program order (two dependent calls always sit in groups i < j), and independent calls
+// of one plan -- the reference's per-stripe loop, even with several plans interleaved per stripe -- share a
+// launch.  Earliest, not latest: in a two-block repair whose second plan reads the block its first plan
+// rebuilt (handle_repair.cpp per plan), every stripe's first plan shares one group and every second plan
+// the next, instead of a new pair of groups per stripe (a launch per stripe).  A call placed before a later
+// group of its key depends on nothing in between, and calls after it see its group in `seen`.
 // reads(c, f) / writes(c, f) call f(address) per block call c reads / writes.  Returns the groups,
 // each listing its calls in program order.
 template <class Key, class Reads, class Writes>
 std::vector<std::vector<size_t>> schedule_groups(size_t n, Key key, Reads reads, Writes writes) {
     std::vector<std::vector<size_t>> groups;
-    std::vector<int> last_of_key;  // key -> latest group index + 1
+    std::vector<std::vector<int>> of_key;  // key -> its groups' index + 1, ascending
     thread_local PtrGroups seen;
     seen.reset(4 * n);
     for (size_t c = 0; c < n; c++) {
@@ -392,12 +396,16 @@ std::vector<std::vector<size_t>> schedule_groups(size_t n, Key key, Reads reads,
         reads(c, [&](const void* p) { lo = std::max(lo, seen.last_write(p)); });
         writes(c, [&](const void* p) { lo = std::max(lo, seen.last_touch(p)); });
         const int kc = key(c);
-        if ((size_t)kc >= last_of_key.size()) last_of_key.resize((size_t)kc + 1, 0);
-        int g1 = last_of_key[kc];
-        if (g1 == 0 || g1 <= lo) {
+        if ((size_t)kc >= of_key.size()) of_key.resize((size_t)kc + 1);
+        std::vector<int>& mine = of_key[(size_t)kc];
+        const auto it = std::upper_bound(mine.begin(), mine.end(), lo);
+        int g1;
+        if (it != mine.end()) {
+            g1 = *it;
+        } else {
             groups.emplace_back();
             g1 = (int)groups.size();
-            last_of_key[kc] = g1;
+            mine.push_back(g1);
         }
         groups[(size_t)g1 - 1].push_back(c);
         reads(c, [&](const void* p) { PtrGroups::Slot& s = seen.at(p); s.rd = std::max(s.rd, g1); });

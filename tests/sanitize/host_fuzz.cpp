@@ -223,8 +223,10 @@ static void grouping() {
                 if (std::count(c[a].wr.begin(), c[a].wr.end(), p) || std::count(c[a].rd.begin(), c[a].rd.end(), p)) return true;
             return false;
         };
-        // quadratic restatement of the join rule, and the legality of the result
-        std::vector<int> ref(n), last(keys, -1);
+        // quadratic restatement of the join rule (the earliest group of the call's key after every group it
+        // depends on, else a new group), and the legality of the result
+        std::vector<int> ref(n);
+        std::vector<std::vector<int>> mine(keys);
         int ng = 0;
         for (int b = 0; b < n; b++) {
             int lo = -1;
@@ -238,8 +240,13 @@ static void grouping() {
                     lo = std::max(lo, ref[a]);
                 }
             }
-            if (last[c[b].key] > lo) ref[b] = last[c[b].key];
-            else ref[b] = last[c[b].key] = ng++;
+            ref[b] = -1;
+            for (int g : mine[c[b].key])
+                if (g > lo) {
+                    ref[b] = g;
+                    break;
+                }
+            if (ref[b] < 0) mine[c[b].key].push_back(ref[b] = ng++);
             if (ref[b] != g_of[b]) {
                 fprintf(stderr, "schedule_groups: call %d in group %d, rule says %d (trial %d)\n", b, g_of[b], ref[b], trial);
                 abort();
