@@ -1392,8 +1392,6 @@ def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
             "dtype": "u8", "data": "synthetic (splitmix64 bytes generated on device)"}
 
 
-# ------------------------------------------------------------------------------- config 5
-
 # ------------------------------------------------------------------------------- every code family
 
 # (name, ECTYPE, coding parameters, the reference's class).  BASELINE's block size, working sets of >= 4 GiB
@@ -1717,6 +1715,8 @@ def families_cpu_leg(t, params, k, m, B, progs, stripes, truth, n, nscr):
                      "class restatement over the C oracle's SIMD region multiply), one thread")
     return res
 
+
+# ------------------------------------------------------------------------------- config 5
 
 def encode_waves(k, m, M, B, first, last, W, seed=0xEC0DE, on_wave=None):
     """Encode global stripes [first, last) of the synthetic RS(k, m) batch in HBM-resident waves of at most

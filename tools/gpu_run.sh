@@ -19,6 +19,8 @@
 #   wp:<name>  rocprofv3 kernel stats of one workload
 #   families   bench.py --workload families (every code class: encode, repairs, decode)   -> families.log
 #   famprof    rocprofv3 kernel trace of the families workload + tools/families_profile.py -> families_profile.json
+#   percall    config 4's per-call merge sequence under launch-option variants (tools/percall_probe.py), one
+#              rocprofv3 kernel trace sliced per variant                           -> percall_summary.json
 #   w34prof    rocprofv3 kernel traces of each form the line's config3 / config4 objects time (one run per
 #              form) -> workload_profile.json (tools/workload_profile.py; copy it to profiles/ for bench.py)
 #   ceiling    tools/movement_ceiling: the product kernel's own access path with the multiply removed, and its
@@ -107,6 +109,11 @@ for step in "$@"; do
     famprof) prof famprof famprof.log --workload families --steps ${FSTEPS:-5} --warmup 2 --no-cpu-baseline ${FARGS:-}
              python tools/families_profile.py "$O/famprof/run_kernel_trace.csv" "$O/famprof.log" \
                "$O/families_profile.json" > "$O/families_profile.log" 2>&1 && echo "families_profile ok" || exit 1 ;;
+    percall) (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace -d "$R/$O/percall" -o run \
+               --output-format csv -- python3 "$R/tools/percall_probe.py" run > "$R/$O/percall.log" 2>&1)
+             rc=$?; echo "percall rc=$rc"; [ $rc -eq 0 ] || exit $rc
+             python tools/percall_probe.py parse "$O/percall/run_kernel_trace.csv" "$O/percall.log" \
+               > "$O/percall_summary.json" 2>&1 && echo "percall summary ok" || exit 1 ;;
     w34prof) C3="fused reference_sequence_scope_scratch reference_sequence_per_call reference_sequence_per_call_threads8"
              C4="rows fused reference_sequence_scope_scratch reference_sequence_per_call"
              spec=""
