@@ -1577,16 +1577,21 @@ def family_rows(a, r, rp, name, t, params, anchor, B, steps, warmup):
             if failed is not None:
                 stripes[fs, fb] = 0xA5
 
+        host = [0.0, 0]  # host seconds inside the replay call (recording + flush; launches are asynchronous)
+
         def fn(ev=None):
             if ev:
                 ev[0].record()
             st = torch.cuda.current_stream().cuda_stream
+            h0 = time.perf_counter()
             rc = rp.ecg_replay_calls(handles, 2, S, 1, stripes.data_ptr(),  # one scope per batch
                                      stripes.stride(0), stripes.stride(1), B, S, pat_of.data_ptr(), prog.data_ptr(),
                                      off.data_ptr(), n, scratch.shape[1], scratch.data_ptr(), st)
             if rc != 0:
                 raise ecg.EcgError(rc, f"ecg_replay_calls({name}, {op})")
             if ev:
+                host[0] += time.perf_counter() - h0
+                host[1] += 1
                 ev[1].record()
 
         poison()
@@ -1612,6 +1617,7 @@ def family_rows(a, r, rp, name, t, params, anchor, B, steps, warmup):
                "launches_per_batch": (c1["launches"] - c0["launches"]) / steps,
                "calls_per_batch": sum(_ncalls(cl[s % npat]) for s in range(S)),
                "launch_range": [c0["launches"], c1["launches"]], "verified": verified,
+               "host_ms_per_batch": round(host[0] / max(1, host[1]) * 1e3, 3),
                "ops_per_s": round(r.world * S * steps / elapsed, 1)}
         if pats is not None:
             row["patterns"] = len(pats)

@@ -13,5 +13,5 @@ for c, cv in line["classes"].items():
         p = prof["classes"].get(c, {}).get(o, {})
         print(f"{c:30s} {o:8s} S={cv['stripes_per_gpu']:4d} ms={v['ms_per_batch']:7.3f} frac={v['frac']:.3f} "
               f"exec/alg={v['executed_over_algorithmic']:.3f} launches={v['launches_per_batch']:5.1f} "
-              f"calls={v['calls_per_batch']:5d} ok={v['verified']} | {p.get('dominant_kernel')} "
+              f"calls={v['calls_per_batch']:5d} host={v.get('host_ms_per_batch')} ok={v['verified']} | {p.get('dominant_kernel')} "
               f"avg={p.get('dominant_avg_us')}us busy={p.get('kernel_busy_frac')}")

@@ -114,6 +114,7 @@ for step in "$@"; do
              rc=$?; echo "percall rc=$rc"; [ $rc -eq 0 ] || exit $rc
              python tools/percall_probe.py parse "$O/percall/run_kernel_trace.csv" "$O/percall.log" \
                > "$O/percall_summary.json" 2>&1 && echo "percall summary ok" || exit 1 ;;
+    percall_plain) run percall_plain 600 "$O/percall_plain.log" python tools/percall_probe.py run ;;
     w34prof) C3="fused reference_sequence_scope_scratch reference_sequence_per_call reference_sequence_per_call_threads8"
              C4="rows fused reference_sequence_scope_scratch reference_sequence_per_call"
              spec=""

@@ -17,8 +17,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "erasure-codes-prototype_amd"))
 
-VARIANTS = [  # name, {option: value}
+VARIANTS = [  # name, {option: value}; "B=..." variants change the block size (merges scaled to >= 8 GiB)
     ("default", {}),
+    ("B=64KiB", {"B": 64 << 10}),
+    ("B=1MiB", {"B": 1 << 20}),
+    ("B=16MiB", {"B": 16 << 20}),
     ("lds_pad_0", {"ECG_OPT_MT1_LDS_PAD": 0}),
     ("lds_pad_24k", {"ECG_OPT_MT1_LDS_PAD": 24576}),
     ("grid_map_0", {"ECG_OPT_GRID_MAP": 0}),
@@ -42,18 +45,21 @@ def run():
     a = types.SimpleNamespace(steps=5, warmup=1, block_size=None, stripes=None, forms=None)
     out = {"what": "pc_merge reference_sequence_per_call, 128 merges x 4 MiB, option variants", "variants": {}}
     for name, opts in VARIANTS:
+        opts = dict(opts)
+        B = opts.pop("B", 4 << 20)
+        S = max(32, (8 << 30) // (50 * B))
         saved = {o: ecg.get_option(getattr(ecg, o)) for o in opts}
         for o, v in opts.items():
             ecg.set_option(getattr(ecg, o), v)
         try:
             c0 = ecg.traffic_counters()
-            res = bench.pc_merge(a, r, only=("reference_sequence_per_call",), S=128, B=4 << 20)
+            res = bench.pc_merge(a, r, only=("reference_sequence_per_call",), S=min(S, 4096), B=B)
             c1 = ecg.traffic_counters()
         finally:
             for o, v in saved.items():
                 ecg.set_option(getattr(ecg, o), v)
         v = res["results"]["reference_sequence_per_call"]
-        out["variants"][name] = {"options": opts, "algorithmic_frac": v["algorithmic_frac"],
+        out["variants"][name] = {"options": opts, "block_size": B, "algorithmic_frac": v["algorithmic_frac"],
                                  "ms_per_batch": v["ms_per_batch"], "launch_range": [c0["launches"], c1["launches"]],
                                  "bytes_per_launch": (c1["bytes"] - c0["bytes"]) / max(1, c1["launches"] - c0["launches"])}
         torch.cuda.empty_cache()
@@ -80,8 +86,14 @@ def parse(trace, log):
         for _, kn, d, _, _ in ks:
             per.setdefault(kn, []).append(d / 1e3)
         gaps = [ks[i + 1][3] - ks[i][4] for i in range(len(ks) - 1)]
-        res[name] = {"event_frac": v["algorithmic_frac"], "launches": len(ks),
+        # the sequence per merged row: helper partial 4 -> 1, main partial 4 -> 1, perform_addition 2 -> 1
+        pos = {}
+        for i, (_, _, d, _, _) in enumerate(ks):
+            pos.setdefault(("helper_4to1", "main_4to1", "addition_2to1")[i % 3], []).append(d / 1e3)
+        res[name] = {"event_frac": v["algorithmic_frac"], "launches": len(ks), "block_size": v.get("block_size"),
                      "median_gap_us": round(statistics.median(gaps) / 1e3, 3) if gaps else None,
+                     "by_call": {p: {"median_us": round(statistics.median(d), 3),
+                                     "p10_us": round(sorted(d)[len(d) // 10], 3)} for p, d in pos.items()},
                      "kernels": {kn: {"n": len(d), "avg_us": round(sum(d) / len(d), 3),
                                       "median_us": round(statistics.median(d), 3), "min_us": round(min(d), 3)}
                                  for kn, d in per.items()}}
