@@ -108,12 +108,14 @@ for step in "$@"; do
                 ${FARGS:-}; tail -c 600 "$O/families.log"; echo ;;
     famprof) prof famprof famprof.log --workload families --steps ${FSTEPS:-5} --warmup 2 --no-cpu-baseline ${FARGS:-}
              python tools/families_profile.py "$O/famprof/run_kernel_trace.csv" "$O/famprof.log" \
-               "$O/families_profile.json" > "$O/families_profile.log" 2>&1 && echo "families_profile ok" || exit 1 ;;
+               "$O/families_profile.json" > "$O/families_profile.log" 2>&1 && echo "families_profile ok" || exit 1
+             rm -f "$O/famprof/run_kernel_trace.csv" ;;  # summarised above; keeps gpurun_out under its copy-back cap
     percall) (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace -d "$R/$O/percall" -o run \
                --output-format csv -- python3 "$R/tools/percall_probe.py" run > "$R/$O/percall.log" 2>&1)
              rc=$?; echo "percall rc=$rc"; [ $rc -eq 0 ] || exit $rc
              python tools/percall_probe.py parse "$O/percall/run_kernel_trace.csv" "$O/percall.log" \
-               > "$O/percall_summary.json" 2>&1 && echo "percall summary ok" || exit 1 ;;
+               > "$O/percall_summary.json" 2>&1 && echo "percall summary ok" || exit 1
+             rm -f "$O/percall/run_kernel_trace.csv" ;;
     percall_plain) run percall_plain 600 "$O/percall_plain.log" python tools/percall_probe.py run ;;
     w34prof) C3="fused reference_sequence_scope_scratch reference_sequence_per_call reference_sequence_per_call_threads8"
              C4="rows fused reference_sequence_scope_scratch reference_sequence_per_call"
