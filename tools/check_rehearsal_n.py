@@ -40,7 +40,7 @@ check("config5 checksum N=1 == N", c5a["parity_checksum"] == c5b["parity_checksu
 check("config5 per-rank shares", len(c5b["stripes_per_rank"]) == n and sum(c5b["stripes_per_rank"]) ==
       sum(c5a["stripes_per_rank"]), c5b["stripes_per_rank"])
 check("config5 hbm_frac_per_rank", len(c5b["hbm_frac_per_rank"]) == n, c5b["hbm_frac_per_rank"])
-for obj in ("ring_repair", "global_ring_repair", "merge_ring", "host_path", "config3", "config4"):
+for obj in ("ring_repair", "global_ring_repair", "merge_ring", "host_path", "config3", "config4", "families"):
     for nm, x in (("N=1", one), (f"N={n}", many)):
         o = x.get(obj, {})
         check(f"{obj} {nm} verified_all_ranks", o.get("verified_all_ranks") is True,
