@@ -19,6 +19,7 @@
 #   wp:<name>  rocprofv3 kernel stats of one workload
 #   families   bench.py --workload families (every code class: encode, repairs, decode)   -> families.log
 #   famprof    rocprofv3 kernel trace of the families workload + tools/families_profile.py -> families_profile.json
+#   fampmc     FETCH_SIZE / WRITE_SIZE passes of the families workload -> families_pmc.json (per row HBM bytes)
 #   percall    config 4's per-call merge sequence under launch-option variants (tools/percall_probe.py), one
 #              rocprofv3 kernel trace sliced per variant                           -> percall_summary.json
 #   w34prof    rocprofv3 kernel traces of each form the line's config3 / config4 objects time (one run per
@@ -116,6 +117,15 @@ for step in "$@"; do
              python tools/percall_probe.py parse "$O/percall/run_kernel_trace.csv" "$O/percall.log" \
                > "$O/percall_summary.json" 2>&1 && echo "percall summary ok" || exit 1
              rm -f "$O/percall/run_kernel_trace.csv" ;;
+    fampmc) for c in FETCH_SIZE WRITE_SIZE; do
+              (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $c -d "$R/$O/fampmc_$c" -o run --output-format csv \
+                 -- python3 "$R/bench.py" --workload families --steps 2 --warmup 1 --no-cpu-baseline ${FARGS:-} \
+                 > "$R/$O/fampmc_$c.log" 2>&1); rc=$?; echo "fampmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+            done
+            python tools/families_pmc.py "$O/fampmc_FETCH_SIZE/**/*counter_collection.csv" "$O/fampmc_FETCH_SIZE.log" \
+              "$O/fampmc_WRITE_SIZE/**/*counter_collection.csv" "$O/fampmc_WRITE_SIZE.log" "$O/families_pmc.json" \
+              > "$O/families_pmc.log" 2>&1 && echo "families pmc ok" || exit 1
+            rm -rf "$O/fampmc_FETCH_SIZE" "$O/fampmc_WRITE_SIZE" ;;
     percall_plain) run percall_plain 600 "$O/percall_plain.log" python tools/percall_probe.py run ;;
     w34prof) C3="fused reference_sequence_scope_scratch reference_sequence_per_call reference_sequence_per_call_threads8"
              C4="rows fused reference_sequence_scope_scratch reference_sequence_per_call"
