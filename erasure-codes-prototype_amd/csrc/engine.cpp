@@ -714,11 +714,45 @@ struct TableSlot {
     void* dev = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
+    hipEvent_t up_ev = nullptr;  // the upload's completion, on the upload stream (upload_table)
     bool pending = false;
 };
 constexpr int kTableSlots = 16;
 TableSlot g_tables[kMaxDevices][kTableSlots];
 std::atomic<unsigned> g_table_next[kMaxDevices];
+
+// Pointer tables go to the device ahead of the launch that reads them.  On the launch's own stream the copy
+// waits for every earlier kernel there and the launch then waits for the copy: a DMA round trip between two
+// kernels.  ECG_TABLE_UPLOAD=1 puts the copy on a per-device upload stream instead, so it runs while the launch
+// stream's earlier kernels do, and the launch waits for it through an event (A/B switch, read once).  The slot's
+// memory is rewritten only after its previous launch completed (TableSlot::ev), which waited for its upload.
+bool table_upload_stream() {
+    static const bool on = getenv("ECG_TABLE_UPLOAD") && atoi(getenv("ECG_TABLE_UPLOAD")) == 1;
+    return on;
+}
+std::mutex g_upload_mu;
+hipStream_t g_upload_stream[kMaxDevices];
+
+hipError_t upload_table(int dev, TableSlot& t, size_t bytes, hipStream_t st) {
+    if (!table_upload_stream()) return hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, st);
+    hipStream_t u;
+    {
+        std::lock_guard<std::mutex> lk(g_upload_mu);
+        if (!g_upload_stream[dev]) {
+            const hipError_t e = hipStreamCreateWithFlags(&g_upload_stream[dev], hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+        }
+        u = g_upload_stream[dev];
+    }
+    hipError_t e;
+    if (!t.up_ev && (e = hipEventCreateWithFlags(&t.up_ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, u)) != hipSuccess) return e;
+    if ((e = hipEventRecord(t.up_ev, u)) != hipSuccess) {
+        (void)hipStreamSynchronize(u);
+        return e;
+    }
+    return hipStreamWaitEvent(st, t.up_ev, 0);
+}
 
 // One side (the inputs or the outputs of `ids`) of a run of recorded calls in the strided form
 // base + call * sstride + v[j] * bstride.  True only if EVERY pointer of every call is exactly that, so
@@ -1856,7 +1890,7 @@ int Engine::run_ptr_batch(const LinearOp& op, const std::vector<const uint8_t* c
         }
         if (apart) apart = outputs_apart(h + (size_t)s * k, k, h + (size_t)S * k + (size_t)s * m, m, B);
     }
-    ECG_HIP(hipMemcpyAsync(t.dev, t.host, n * sizeof(void*), hipMemcpyHostToDevice, st));
+    ECG_HIP(upload_table(device_, t, n * sizeof(void*), st));
     const uint8_t* const* d_src = (const uint8_t* const*)t.dev;
     uint8_t* const* d_dst = (uint8_t* const*)((const uint8_t**)t.dev + (size_t)S * k);
     const int rc = run_ptrs(op, d_src, d_dst, S, B, aligned, st, apart);
@@ -1978,7 +2012,7 @@ int Engine::run_ptr_batch_multi(const std::vector<const LinearOp*>& ops, const s
         if (apart) apart = outputs_apart(h + (size_t)c * k, k, h + (size_t)S * k + (size_t)c * m, m, B);
         hp[c] = pid[c];
     }
-    ECG_HIP(hipMemcpyAsync(t.dev, t.host, bytes, hipMemcpyHostToDevice, st));
+    ECG_HIP(upload_table(device_, t, bytes, st));
     GfLaunch a;
     memset(&a, 0, sizeof(a));
     a.tabs = ps->d_tabs;
