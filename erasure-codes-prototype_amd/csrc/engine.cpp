@@ -1514,6 +1514,9 @@ int batch_flush() {
     d.last_dev = prev_dev;
     d.last_recorded = prev_recorded;
     d.stats = st;
+    // the next recording reuses this queue's capacity (a scope of thousands of calls regrew it every flush)
+    q.clear();
+    if (d.q.empty() && d.q.capacity() < q.capacity()) d.q.swap(q);
     return rc;
 }
 
