@@ -13,6 +13,7 @@
 #include "ecg.h"
 #include "engine.hpp"  // ecg::schedule_groups, ecg::compose_scratch (pure host logic of the batch-scope flush)
 #include "gf256.hpp"
+#include "matrix.hpp"  // ecg::compose_chain
 
 static std::mt19937_64 rng(12345);
 static int rnd(int lo, int hi) { return std::uniform_int_distribution<int>(lo, hi)(rng); }
@@ -434,6 +435,63 @@ static void scratch_composition() {
 // addresses.  Only where no GPU exists: the flush then stops at its first launch with ECG_EHIP (a
 // program-table allocation), so only the first group is launched; the grouping of every flush is
 // covered by grouping() above.  With a GPU the fake addresses would be launched.
+// Chain composition (ecg::compose_chain, the facade's product-code plans) against running the chain op by op:
+// random chains over a small block-id space -- ops reading blocks earlier ops wrote, rewriting blocks, 0 / 1 /
+// general coefficients, cancelling terms -- on random bytes.  Where compose_chain gives one op, that op over the
+// original blocks must leave every block as the chain does; where it refuses, the chain must really need its
+// order (a written block's original bytes feed a final value) or every final value is zero.
+static void chains() {
+    long long composed = 0, refused = 0;
+    const int L = 37;
+    for (int trial = 0; trial < 20000; trial++) {
+        const int nb = rnd(2, 12), nops = rnd(1, 6);
+        std::vector<ecg::LinearOp> ops(nops);
+        for (auto& op : ops) {  // destinations, then sources from the other blocks: an op never reads what it writes
+            std::vector<int> ids(nb);
+            for (int i = 0; i < nb; i++) ids[i] = i;
+            std::shuffle(ids.begin(), ids.end(), rng);
+            const int m = rnd(1, std::min(4, nb - 1)), k = rnd(1, nb - m);
+            op.dst_ids.assign(ids.begin(), ids.begin() + m);
+            op.src_ids.assign(ids.begin() + m, ids.begin() + m + k);
+            op.coef.resize(op.src_ids.size() * op.dst_ids.size());
+            const int flavour = rnd(0, 2);
+            for (auto& c : op.coef) c = (uint8_t)(flavour == 0 ? rnd(0, 1) : flavour == 1 ? rnd(0, 255) : (rnd(0, 3) ? 1 : rnd(2, 255)));
+        }
+        std::vector<std::vector<uint8_t>> seq(nb, std::vector<uint8_t>(L));
+        for (auto& b : seq)
+            for (auto& x : b) x = (uint8_t)rnd(0, 255);
+        const std::vector<std::vector<uint8_t>> orig = seq;
+        auto apply = [&](const ecg::LinearOp& op, const std::vector<std::vector<uint8_t>>& in,
+                         std::vector<std::vector<uint8_t>>& out) {
+            std::vector<std::vector<uint8_t>> rows(op.m_out(), std::vector<uint8_t>(L, 0));
+            for (int p = 0; p < op.m_out(); p++)
+                for (int j = 0; j < op.k_in(); j++)
+                    for (int x = 0; x < L; x++)
+                        rows[p][x] ^= (uint8_t)ecg::gf::mul(op.coef[(size_t)p * op.k_in() + j], in[op.src_ids[j]][x]);
+            for (int p = 0; p < op.m_out(); p++) out[op.dst_ids[p]] = rows[p];
+        };
+        for (const auto& op : ops) apply(op, seq, seq);
+        ecg::LinearOp one;
+        if (!ecg::compose_chain(ops, one)) {
+            refused++;
+            continue;
+        }
+        composed++;
+        for (int s : one.src_ids)
+            if (std::find(one.dst_ids.begin(), one.dst_ids.end(), s) != one.dst_ids.end()) {
+                fprintf(stderr, "compose_chain: composed op reads a block it writes (trial %d)\n", trial);
+                abort();
+            }
+        std::vector<std::vector<uint8_t>> got = orig;
+        apply(one, orig, got);
+        if (got != seq) {
+            fprintf(stderr, "compose_chain: composed op differs from the chain (trial %d)\n", trial);
+            abort();
+        }
+    }
+    printf("chains: %lld composed and checked, %lld left as chains\n", composed, refused);
+}
+
 static void batch_scope() {
     if (ecg_device_count() > 0) return;
     ecg_coding_parameters cp{};
@@ -465,6 +523,7 @@ int main() {
     decode_plans();
     grouping();
     scratch_composition();
+    chains();
     batch_scope();
     printf("host fuzz done\n");
     return 0;
