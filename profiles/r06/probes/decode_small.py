@@ -1,5 +1,5 @@
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "erasure-codes-prototype_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "..", "erasure-codes-prototype_amd"))
 import numpy as np
 import torch
 import ecg

@@ -1,5 +1,5 @@
 import sys, os
-ROOT = os.path.join(os.path.dirname(__file__), "..", "..")
+ROOT = os.path.join(os.path.dirname(__file__), "..", "..", "..")
 sys.path.insert(0, os.path.join(ROOT, "erasure-codes-prototype_amd"))
 sys.path.insert(0, ROOT)
 import numpy as np
