@@ -41,7 +41,7 @@ mkdir -p "$O"
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 PYT="python -u -m pytest -p no:cacheprovider --timeout 120 --timeout-method thread"
-HEADLINE="--no-config5 --no-ring --no-host-path --no-configs34"
+HEADLINE="--no-config5 --no-ring --no-host-path --no-configs34 --no-families"
 
 run() {  # name limit log cmd...  (the command's output goes to log; the status line to this script's stdout)
   local name=$1 lim=$2 log=$3; shift 3
