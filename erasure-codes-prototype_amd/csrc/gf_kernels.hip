@@ -215,6 +215,13 @@ __device__ __forceinline__ int launch_prog(const GfLaunch& a, int& s) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Input blocks whose loads a lane keeps in flight before folding them (ECG_TUNE_LOAD_BATCH: tuning builds only).
+#ifdef ECG_TUNE_LOAD_BATCH
+constexpr int kLoadBatch = ECG_TUNE_LOAD_BATCH;
+#else
+constexpr int kLoadBatch = 4;
+#endif
+
 // Generic vector path: bytes [0, 16 * floor(B / 16)) of every block; all pointers 16-byte aligned.
 // grid.x = S * wg_per_stripe (stripe-major), grid.y = row tiles of MT outputs.
 template <int MT, int MODE, int NT, bool BIN>
@@ -266,11 +273,21 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
                 j = k;
             }
         }
-        for (; j + 4 <= k; j += 4) {
-            uint32_t x[4][4];
+        constexpr int LB = BIN ? kLoadBatch : 4;  // GENERAL tiles spill above 4 under their occupancy hints
+        for (; j + LB <= k; j += LB) {
+            uint32_t x[LB][4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) load16<NT>(src_ptr<MODE>(a, s, prog, j + u) + off, x[u]);
-            fold<MT, 4, BIN>(x, T + (size_t)j * MT, acc);
+            for (int u = 0; u < LB; ++u) load16<NT>(src_ptr<MODE>(a, s, prog, j + u) + off, x[u]);
+            fold<MT, LB, BIN>(x, T + (size_t)j * MT, acc);
+        }
+        if constexpr (LB > 4) {
+            if (j + 4 <= k) {
+                uint32_t x[4][4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) load16<NT>(src_ptr<MODE>(a, s, prog, j + u) + off, x[u]);
+                fold<MT, 4, BIN>(x, T + (size_t)j * MT, acc);
+                j += 4;
+            }
         }
         if (j + 2 <= k) {
             uint32_t x[2][4];
