@@ -208,7 +208,7 @@ def timed_loop(r, steps, step):
 
 def warm_for(fn, count, seconds=0.03, chunk=4):
     """At least `count` untimed calls of fn, and more, `chunk` at a time with a synchronize after each, until
-    `seconds` of wall time have passed.  A row that follows host-only work (the previous class's oracle check, a
+    `seconds` of wall time have passed; returns the calls made.  A row that follows host-only work (the previous class's oracle check, a
     few seconds) starts on an idle GPU, and two 1 ms batches do not bring its clocks back: the first rows of the
     families line ran 3-8 % below the same launch run back to back."""
     t0 = time.perf_counter()
@@ -218,6 +218,7 @@ def warm_for(fn, count, seconds=0.03, chunk=4):
             fn()
         i += chunk
         torch.cuda.synchronize()
+    return i
 
 
 def pipelined_loop(r, steps, step):
@@ -995,16 +996,14 @@ def lrc_repair(a, r, only=None, steps=None, warmup=None, S=None, B=None):
     for name, make, executed in forms:
         fn = make()
         rebuilt.zero_()
-        for _ in range(warmup):
-            fn()
-        torch.cuda.synchronize()
+        warmed = warm_for(fn, warmup)
         assert torch.equal(rebuilt[:, 0], stripes[idx, e_of.long()]), f"{name}: repair mismatch"
         elapsed, evs = pipelined_loop(r, steps, fn)
         t = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
         res = {"repairs_per_s": round(r.world * S * (steps + 1) / elapsed, 1), "ms_per_batch": round(t * 1e3, 3),
                "algorithmic_GBps": round(alg / t / 1e9, 1), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
                "verified": True,  # every repaired block equal to the lost one (the assert above)
-               "batches_run": warmup + steps + 1}
+               "batches_run": warmed + steps + 1}
         if name == "reference_sequence_scope_scratch":
             st = replay_stats[2]  # the last scope's flush: 3 recorded calls per repair, composed to 1
             res["last_scope_flush"] = st
@@ -1377,9 +1376,7 @@ def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
                 ev[1].record()
 
         out.zero_()
-        for _ in range(warmup):
-            step()
-        torch.cuda.synchronize()
+        warmed = warm_for(step, warmup)
         for s in (0, S // 2 + 1, S - 1):  # merges checked against XOR on the host
             hb = blocks[s].cpu().numpy()
             for row in range(5):
@@ -1422,7 +1419,7 @@ def pc_merge(a, r, only=None, steps=None, warmup=None, S=None, B=None):
                      "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
                      "executed_bytes_per_batch": executed,
                      "executed_frac": round(executed / t / 1e9 / HBM_PEAK_GBS, 4) if executed else None,
-                     **extra, "verified": True, "batches_run": warmup + steps + 1}
+                     **extra, "verified": True, "batches_run": warmed + steps + 1}
         del fn
     return {"workload": "PC(4,1,4,1) merge x=2 horizontal, 4 MiB blocks", "n_gpus": r.world,
             "merges_per_gpu": S, "steps": steps, "algorithmic_bytes_per_batch": alg, "results": res,

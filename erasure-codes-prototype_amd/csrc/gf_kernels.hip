@@ -163,7 +163,8 @@ __device__ __forceinline__ void fold(const uint32_t (&x)[U][4], const ECG_CONST 
 // Minimum waves per EU the register allocator must allow (r01 sweep, tools/gpu_variants.sh): 8 for the
 // 1-2-output kernels (decode, repair, XOR: +2 % at 8 vs 6), 6 for 3-4 outputs (encode: 8 costs 1 %),
 // 4 above -- except 5 outputs: under the 128-VGPR cap of 4 waves the allocator spilled 12 bytes per lane
-// in the GENERAL flavour, while a hint of 3 lets it settle at 82 VGPRs (5 waves) with no scratch.
+// in the GENERAL flavour, while a hint of 3 lets it settle at 82 VGPRs (5 waves) with no scratch (r01; with
+// two inputs per load batch since r06 it takes 61, 7 waves).
 // ECG_OCC_OVERRIDE is for tuning builds only.
 constexpr int occupancy_for(int MT) {
 #ifdef ECG_OCC_OVERRIDE
@@ -221,6 +222,20 @@ constexpr int kLoadBatch = ECG_TUNE_LOAD_BATCH;
 #else
 constexpr int kLoadBatch = 4;
 #endif
+// GENERAL tiles of 5+ outputs take two: with four, 4 inputs x MT tables (5 dwords each) outgrow the SGPR file and the
+// tile needs 87 VGPRs at MT = 5 (5 waves per SIMD); with two it takes 61 (7 waves), and a 12 -> 5 launch (the
+// Azure+1 encode) runs 0.745 of 8 TB/s instead of 0.684-0.694, 12 -> 6 0.70 instead of 0.66, 10 -> 8 0.665 instead
+// of 0.61 (profiles/r06/families/shape_probe/sp_glb*.log, two processes each).
+#ifdef ECG_TUNE_GEN_WIDE_LB
+constexpr int kGenWideLB = ECG_TUNE_GEN_WIDE_LB;
+#else
+constexpr int kGenWideLB = 2;
+#endif
+#ifdef ECG_TUNE_GEN_LB
+constexpr int kGenLB = ECG_TUNE_GEN_LB;  // GENERAL tiles of 1-4 outputs (tuning builds only)
+#else
+constexpr int kGenLB = 4;
+#endif
 
 // Generic vector path: bytes [0, 16 * floor(B / 16)) of every block; all pointers 16-byte aligned.
 // grid.x = S * wg_per_stripe (stripe-major), grid.y = row tiles of MT outputs.
@@ -273,14 +288,14 @@ __global__ void __launch_bounds__(kThreads, MODE == GF_MODE_INLINE_LAT ? 1 : occ
                 j = k;
             }
         }
-        constexpr int LB = BIN ? kLoadBatch : 4;  // GENERAL tiles spill above 4 under their occupancy hints
+        constexpr int LB = BIN ? kLoadBatch : MT >= 5 ? kGenWideLB : kGenLB;
         for (; j + LB <= k; j += LB) {
             uint32_t x[LB][4];
 #pragma unroll
             for (int u = 0; u < LB; ++u) load16<NT>(src_ptr<MODE>(a, s, prog, j + u) + off, x[u]);
             fold<MT, LB, BIN>(x, T + (size_t)j * MT, acc);
         }
-        if constexpr (LB > 4) {
+        if constexpr (LB > 4) {  // the rest of k: four, two, one
             if (j + 4 <= k) {
                 uint32_t x[4][4];
 #pragma unroll
