@@ -208,9 +208,10 @@ def timed_loop(r, steps, step):
 
 def warm_for(fn, count, seconds=0.03, chunk=4):
     """At least `count` untimed calls of fn, and more, `chunk` at a time with a synchronize after each, until
-    `seconds` of wall time have passed; returns the calls made.  A row that follows host-only work (the previous class's oracle check, a
-    few seconds) starts on an idle GPU, and two 1 ms batches do not bring its clocks back: the first rows of the
-    families line ran 3-8 % below the same launch run back to back."""
+    `seconds` of wall time have passed; returns the calls made.  A row that follows host-side setup (a class's
+    repair plans, its decode dependency probe, the previous class's oracle check) starts on a nearly idle GPU,
+    and two 1 ms batches did not bring its clocks back: the families encodes ran 3-15 % below the same launch
+    run back to back."""
     t0 = time.perf_counter()
     i = 0
     while i < count or time.perf_counter() - t0 < seconds:
