@@ -723,9 +723,13 @@ def test_fill_random_matches_oracle(ecg, oracle, torch_cuda):
         assert np.array_equal(t.cpu().numpy(), oracle.splitmix_bytes(0xEC0DE, off, n))
 
 
-def test_encode_batch_vs_oracle(ecg, oracle, torch_cuda):
+@pytest.mark.parametrize("k,m,B,S", [(10, 4, 1 << 20, 6), (13, 5, 65536 + 40, 5), (9, 7, 65536 + 40, 3),
+                                     (3, 9, 4096 + 8, 4), (11, 12, 4096 + 8, 3)])
+def test_encode_batch_vs_oracle(ecg, oracle, torch_cuda, k, m, B, S):
+    """Strided batched encodes: the headline shape, and GENERAL tiles of 5+ outputs (two inputs per load batch)
+    with odd input counts -- the single-input tail after the pairs -- and two row tiles (m = 9, 12), with byte
+    tails (B % 16 != 0 goes to the byte kernel)."""
     torch = torch_cuda
-    k, m, B, S = 10, 4, 1 << 20, 6
     M = oracle.reed_sol_vandermonde_coding_matrix(k, m)
     d_in = torch.empty((S, k, B), dtype=torch.uint8, device="cuda")
     ecg.fill_random(d_in, 7)
