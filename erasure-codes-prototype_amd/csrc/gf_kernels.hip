@@ -768,7 +768,7 @@ hipError_t launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
 // inputs +2-6 % at 22-24 KiB; one step past each value the rate falls off a cliff (a 1 -> 1 copy already
 // at 12 KiB: 0.80 -> 0.69, so it takes none).  Six-input pointer-table launches (config 3's scope flushes)
 // do best one step higher than strided ones (+1.2-1.5 %, sweep_c3_box2.log, box3/sweep_c3.log).
-// Multi-output launches (the encode) lose at every pad and take none.
+// Launches of 3+ outputs (the encode) lose at every pad and take none; two-output launches: mt2_lds_pad.
 unsigned mt1_lds_pad(int k, bool ptrs) {
     const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
     if (opt >= 0) return (unsigned)opt;
@@ -781,9 +781,29 @@ unsigned mt1_lds_pad(int k, bool ptrs) {
     return 24576;
 }
 
+// Two-output launches (2-block repairs and 2-erasure decodes) take the same kind of cap once they read 8 or more
+// inputs: pointer-table launches, both flavours, two processes each (profiles/r06/families/shape_probe/sp_pad2_*.log):
+// 12 -> 2 0.722 -> 0.734-0.748 at 24 KiB, 20 -> 2 0.700-0.707 -> 0.725-0.727, 30 -> 2 0.702-0.710 -> 0.740-0.751,
+// BINARY 12 / 16 -> 2 +2.5-3 %; 8-10 inputs +1-1.5 % at 20 KiB; 6 inputs none, and 28 KiB already falls off there.
+// (Round 5 measured 0-2 % at 16-20 KiB on 10-input decodes and kept none.)  ECG_TUNE_PAD_MT2 builds take
+// ECG_OPT_MT1_LDS_PAD for them too (tuning only).
+unsigned mt2_lds_pad(int k) {
+#ifdef ECG_TUNE_PAD_MT2
+    const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
+    if (opt >= 0) return (unsigned)opt;
+#endif
+    return k <= 7 ? 0u : k <= 11 ? 20480u : 24576u;
+}
+
 template <int MT, int MODE, int NT, bool BIN>
 hipError_t gen_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
-    const unsigned lds = MT == 1 ? mt1_lds_pad(a.k, MODE == GF_MODE_PTRS) : 0u;
+#ifdef ECG_TUNE_PAD_MT34  // tuning builds only: ECG_OPT_MT1_LDS_PAD caps 3-4-output launches too
+    if constexpr (MT == 3 || MT == 4) {
+        const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
+        return launch_kernel_lds(gf_vec_kernel<MT, MODE, NT, BIN>, g, dim3(kThreads), opt > 0 ? (unsigned)opt : 0u, st, a);
+    }
+#endif
+    const unsigned lds = MT == 1 ? mt1_lds_pad(a.k, MODE == GF_MODE_PTRS) : MT == 2 ? mt2_lds_pad(a.k) : 0u;
     return launch_kernel_lds(gf_vec_kernel<MT, MODE, NT, BIN>, g, dim3(kThreads), lds, st, a);
 }
 

@@ -8,6 +8,8 @@
 #   bench      default bench line (python bench.py)                               -> bench.log
 #   headline   bench line of the headline alone (no config 5 / ring / host path)  -> bench_headline.log
 #   prof       rocprofv3 --kernel-trace --stats of the default line and of the headline alone
+#   profh      the headline alone only (r06: the default line under rocprofv3 once died in the HIP runtime,
+#              SIGSEGV inside hipLaunchKernel, during config 3's 8-thread per-call form)
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the headline -> pmc_traffic.json (tools/parse_pmc.py)
 #   summary    tools/profile_summary.py over prof_headline's trace + pmc_traffic.json -> headline_profile.json
 #              (copy it and pmc_traffic.json to profiles/ to have bench.py's roofline name them)
@@ -86,6 +88,7 @@ for step in "$@"; do
     prof) prof prof prof.log --steps 40 --warmup 3 --no-cpu-baseline
           rm -f "$O/prof/run_kernel_trace.csv"  # 10^5 rows (config 3's per-call forms): the stats stay
           prof prof_headline prof_headline.log --steps 40 --warmup 3 --no-cpu-baseline $HEADLINE ;;
+    profh) prof prof_headline prof_headline.log --steps 40 --warmup 3 --no-cpu-baseline $HEADLINE ;;
     pmc) pmc FETCH_SIZE fetch; pmc WRITE_SIZE write
          python tools/parse_pmc.py "$O/pmc_fetch/**/*counter_collection.csv" "$O/pmc_write/**/*counter_collection.csv" \
            "$O/pmc_traffic.json" rs104_B1048576_S4096 > /dev/null && echo "pmc parse ok" || exit 1 ;;

@@ -34,7 +34,7 @@ using ecg::GfLaunch;
 
 struct Setting {
     const char* name;
-    long long map, group, cols, nt = 3;
+    long long map, group, cols, nt = 3, pad = -1;
 };
 
 struct Case {
@@ -44,6 +44,7 @@ struct Case {
     CoefTab* tabs = nullptr;
     int* src = nullptr;
     int* dst = nullptr;
+    uint8_t** ptrs = nullptr;  // SHAPE_PROBE_MODE=ptrs: [S][k] input then [S][m] output pointers
     std::vector<std::vector<double>> ms;  // per setting
 };
 
@@ -55,11 +56,16 @@ int main(int argc, char** argv) {
     const int rounds = atoi(argv[1]), reps = atoi(argv[2]);
     const long long B = 1LL << 20;
     // SHAPE_PROBE_SET=maps: grid maps only (the auto rule's choice for outputs in the stripes is map 1);
-    // SHAPE_PROBE_SET=nt: the non-temporal policies under the auto map; SHAPE_PROBE_SET=auto: the auto rule only
+    // SHAPE_PROBE_SET=nt: the non-temporal policies under the auto map; SHAPE_PROBE_SET=auto: the auto rule only;
+    // SHAPE_PROBE_SET=pads: LDS pads (workgroups per CU).  SHAPE_PROBE_MODE=ptrs: pointer-table launches.
     const char* set = getenv("SHAPE_PROBE_SET");
     const std::vector<Setting> st =
         set && std::string(set) == "auto"
             ? std::vector<Setting>{{"auto", 3, 1, 0}}
+        : set && std::string(set) == "pads"  // ECG_OPT_MT1_LDS_PAD (2-output launches too in ECG_TUNE_PAD_MT2 builds)
+            ? std::vector<Setting>{{"pad 0", 3, 1, 0, 3, 0},          {"pad 16K", 3, 1, 0, 3, 16384},
+                                   {"pad 20K", 3, 1, 0, 3, 20480},    {"pad 24K", 3, 1, 0, 3, 24576},
+                                   {"pad 28K", 3, 1, 0, 3, 28672}}
         : set && std::string(set) == "maps"
             ? std::vector<Setting>{{"map1", 1, 1, 0}, {"map2 G=1", 2, 1, 0}, {"map2 G=2", 2, 2, 0}, {"map0", 0, 1, 0}}
         : set && std::string(set) == "nt"  // non-temporal policy: bit 0 loads, bit 1 stores (MT <= 8 only)
@@ -102,9 +108,20 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(c.tabs, tabs.data(), tabs.size() * sizeof(CoefTab), hipMemcpyHostToDevice));
         CK(hipMemcpy(c.src, src.data(), src.size() * sizeof(int), hipMemcpyHostToDevice));
         CK(hipMemcpy(c.dst, dst.data(), dst.size() * sizeof(int), hipMemcpyHostToDevice));
+        std::vector<uint8_t*> pt((size_t)c.S * (c.k + c.m));
+        for (int s_ = 0; s_ < c.S; s_++) {
+            uint8_t* base = c.arena + (size_t)s_ * (c.k + c.m) * B;
+            for (int j = 0; j < c.k; j++) pt[(size_t)s_ * c.k + j] = base + (size_t)j * B;
+            for (int p = 0; p < c.m; p++) pt[(size_t)c.S * c.k + (size_t)s_ * c.m + p] = base + (size_t)(c.k + p) * B;
+        }
+        CK(hipMalloc(&c.ptrs, pt.size() * sizeof(uint8_t*)));
+        CK(hipMemcpy(c.ptrs, pt.data(), pt.size() * sizeof(uint8_t*), hipMemcpyHostToDevice));
         c.ms.resize(st.size());
     }
     CK(hipDeviceSynchronize());
+    const char* md = getenv("SHAPE_PROBE_MODE");
+    const bool ptrs_mode = md && std::string(md) == "ptrs";
+    printf("mode %s\n", ptrs_mode ? "PTRS (pointer tables, outputs apart)" : "STRIDED");
     auto launch = [&](const Case& c) {
         GfLaunch a;
         memset(&a, 0, sizeof(a));
@@ -122,7 +139,14 @@ int main(int argc, char** argv) {
         a.MT = c.m;
         a.rtiles = 1;
         a.binary = c.bin;
-        CK(ecg::launch_gf(a, ecg::GF_MODE_STRIDED, true, nullptr));
+        if (ptrs_mode) {  // as the engine issues a batch scope's repairs: outputs apart from the inputs -> grid map 2
+            a.src_ptrs = (const uint8_t* const*)c.ptrs;
+            a.dst_ptrs = (uint8_t* const*)(c.ptrs + (size_t)c.S * c.k);
+            a.grid_map = 2;
+            CK(ecg::launch_gf(a, ecg::GF_MODE_PTRS, true, nullptr));
+        } else {
+            CK(ecg::launch_gf(a, ecg::GF_MODE_STRIDED, true, nullptr));
+        }
     };
     std::vector<hipEvent_t> ev(reps + 1);
     for (auto& e : ev) CK(hipEventCreate(&e));
@@ -133,6 +157,7 @@ int main(int argc, char** argv) {
                 ecg::set_option(ECG_OPT_MAP_GROUP, st[si].group);
                 ecg::set_option(ECG_OPT_COLS_PER_WG, st[si].cols);
                 ecg::set_option(ECG_OPT_NT, st[si].nt);
+                ecg::set_option(ECG_OPT_MT1_LDS_PAD, st[si].pad);
                 for (int w = 0; w < 2; w++) launch(c);
                 CK(hipEventRecord(ev[0], nullptr));
                 for (int i = 0; i < reps; i++) {
