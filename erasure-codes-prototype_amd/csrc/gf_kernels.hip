@@ -768,7 +768,8 @@ hipError_t launch_with(F kernel, const GfLaunch& a, dim3 grid, hipStream_t st) {
 // inputs +2-6 % at 22-24 KiB; one step past each value the rate falls off a cliff (a 1 -> 1 copy already
 // at 12 KiB: 0.80 -> 0.69, so it takes none).  Six-input pointer-table launches (config 3's scope flushes)
 // do best one step higher than strided ones (+1.2-1.5 %, sweep_c3_box2.log, box3/sweep_c3.log).
-// Launches of 3+ outputs (the encode) lose at every pad and take none; two-output launches: mt2_lds_pad.
+// GENERAL launches of 3+ outputs (the encode) lose at every pad and take none; two-output launches: mt2_lds_pad;
+// BINARY tiles of 8-9 outputs: gen_launch.
 unsigned mt1_lds_pad(int k, bool ptrs) {
     const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
     if (opt >= 0) return (unsigned)opt;
@@ -797,13 +798,20 @@ unsigned mt2_lds_pad(int k) {
 
 template <int MT, int MODE, int NT, bool BIN>
 hipError_t gen_launch(const GfLaunch& a, dim3 g, hipStream_t st) {
-#ifdef ECG_TUNE_PAD_MT34  // tuning builds only: ECG_OPT_MT1_LDS_PAD caps 3-4-output launches too
-    if constexpr (MT == 3 || MT == 4) {
+#ifdef ECG_TUNE_PAD_MT_LO  // tuning builds only: ECG_OPT_MT1_LDS_PAD caps launches of MT_LO..MT_HI outputs too
+    if constexpr (MT >= ECG_TUNE_PAD_MT_LO && MT <= ECG_TUNE_PAD_MT_HI) {
         const long long opt = g_opt[ECG_OPT_MT1_LDS_PAD].load(std::memory_order_relaxed);
         return launch_kernel_lds(gf_vec_kernel<MT, MODE, NT, BIN>, g, dim3(kThreads), opt > 0 ? (unsigned)opt : 0u, st, a);
     }
 #endif
-    const unsigned lds = MT == 1 ? mt1_lds_pad(a.k, MODE == GF_MODE_PTRS) : MT == 2 ? mt2_lds_pad(a.k) : 0u;
+    // BINARY tiles of 8-9 outputs (the composed PC / HPC / HVPC encodes, 16 -> 9 and 16 -> 8) run at 8 waves per
+    // SIMD on 52-56 VGPRs and stream 24-25 blocks per workgroup; from 12 inputs a 20 KiB cap is +1.5-2.3 % (16 -> 9
+    // in four of four runs, 16 -> 8, 12 -> 8; profiles/r06/families/shape_probe/sp_padw_*.log).  Wider BINARY tiles
+    // (16 -> 16: 85 VGPRs, 5 waves) and GENERAL tiles of 3+ outputs lose under any cap.
+    constexpr bool kWideBinCap = BIN && (MT == 8 || MT == 9);
+    const unsigned lds = MT == 1 ? mt1_lds_pad(a.k, MODE == GF_MODE_PTRS)
+                         : MT == 2 ? mt2_lds_pad(a.k)
+                         : (kWideBinCap && a.k >= 12) ? 20480u : 0u;
     return launch_kernel_lds(gf_vec_kernel<MT, MODE, NT, BIN>, g, dim3(kThreads), lds, st, a);
 }
 

@@ -117,7 +117,8 @@ long long ecg_host_pinned_xfer_threshold(void);
                                   workgroups share a CU.  -1 = by input count (default: 12-24 KiB, 2-6 %
                                   faster for 8-16 inputs, profiles/r05/occupancy/); 0 = no cap; else that
                                   many bytes, at most 65536.  Two-output launches take a fixed cap by input
-                                  count (20-24 KiB from 8 inputs, profiles/r06/families/shape_probe/) */
+                                  count (20-24 KiB from 8 inputs), and BINARY launches of 8-9 outputs 20 KiB
+                                  from 12 inputs (profiles/r06/families/shape_probe/) */
 #define ECG_OPT_COUNT 11
 int ecg_set_option(int option, long long value);
 long long ecg_get_option(int option);
