@@ -45,6 +45,7 @@ struct Case {
     int* src = nullptr;
     int* dst = nullptr;
     uint8_t** ptrs = nullptr;  // SHAPE_PROBE_MODE=ptrs: [S][k] input then [S][m] output pointers
+    int* prog_of = nullptr;    // SHAPE_PROBE_PROGS=N: N coefficient matrices, stripe s runs prog_of[s]
     std::vector<std::vector<double>> ms;  // per setting
 };
 
@@ -93,12 +94,24 @@ int main(int argc, char** argv) {
         if (al && std::string(al) == "contig") CK(hipExtMallocWithFlags((void**)&c.arena, bytes, hipDeviceMallocContiguous));
         else CK(hipMalloc(&c.arena, bytes));
         CK(ecg::launch_fill_splitmix(c.arena, (long long)bytes, 0xEC0DE, 0, nullptr));
-        std::vector<CoefTab> tabs((size_t)c.k * c.m);
-        for (int j = 0; j < c.k; j++)
-            for (int p = 0; p < c.m; p++) {
-                rng = rng * 1103515245u + 12345u;
-                ecg::make_coef_tab(c.bin ? 1 : 1 + (int)((rng >> 16) % 255), &tabs[(size_t)j * c.m + p]);
-            }
+        // SHAPE_PROBE_PROGS=N[,sorted]: N programs (the matrices of a scope's per-pattern repairs), dealt to the
+        // stripes round robin (s % N, as per-stripe patterns arrive) or sorted (runs of S / N stripes)
+        const char* pe = getenv("SHAPE_PROBE_PROGS");
+        const int nprog = pe ? std::max(1, atoi(pe)) : 1;
+        const bool sorted = pe && strstr(pe, "sorted");
+        std::vector<CoefTab> tabs((size_t)nprog * c.k * c.m);
+        for (int q = 0; q < nprog; q++)
+            for (int j = 0; j < c.k; j++)
+                for (int p = 0; p < c.m; p++) {
+                    rng = rng * 1103515245u + 12345u;
+                    ecg::make_coef_tab(c.bin ? 1 : 1 + (int)((rng >> 16) % 255), &tabs[((size_t)q * c.k + j) * c.m + p]);
+                }
+        if (nprog > 1) {
+            std::vector<int> po(c.S);
+            for (int s_ = 0; s_ < c.S; s_++) po[s_] = sorted ? (int)((long long)s_ * nprog / c.S) : s_ % nprog;
+            CK(hipMalloc(&c.prog_of, po.size() * sizeof(int)));
+            CK(hipMemcpy(c.prog_of, po.data(), po.size() * sizeof(int), hipMemcpyHostToDevice));
+        }
         std::vector<int> src(c.k), dst(c.m);
         for (int j = 0; j < c.k; j++) src[j] = j;
         for (int p = 0; p < c.m; p++) dst[p] = c.k + p;
@@ -139,6 +152,7 @@ int main(int argc, char** argv) {
         a.MT = c.m;
         a.rtiles = 1;
         a.binary = c.bin;
+        a.prog_of_stripe = c.prog_of;
         if (ptrs_mode) {  // as the engine issues a batch scope's repairs: outputs apart from the inputs -> grid map 2
             a.src_ptrs = (const uint8_t* const*)c.ptrs;
             a.dst_ptrs = (uint8_t* const*)(c.ptrs + (size_t)c.S * c.k);
